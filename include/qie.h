@@ -1,0 +1,186 @@
+/*
+ * qie.h -- C ABI of libqie.so, the MI355X (gfx950) hot-path kernels of the
+ * Qwen-Image-Edit-2509 denoise loop (DiT forward + batched CFG + stream batch).
+ *
+ * The reference (shi3z/Qwen-Image-Edit-StreamDiffusion) has no native code: its
+ * hot path is the un-vendored diffusers QwenImageEditPlusPipeline /
+ * QwenImageTransformer2DModel [U], called at server.py:137-153,
+ * qwen_realtime.py:247-255 and benchmark_lightning.py:41-49, and swapped as a
+ * module at benchmark_compile.py:102-106 (`pipeline.transformer = ...`).  Each
+ * entry point below names the upstream operation it replaces inside that call
+ * (SURVEY.md §2D kernel table K1..K14, §8 rows a1..a18).
+ *
+ * Conventions (SURVEY.md §8 b):
+ *   - bf16 tensors are raw 16-bit words; every pointer is device memory owned by
+ *     the caller (PyTorch caching allocator).  The library never allocates,
+ *     frees or synchronises, and keeps no mutable global state.
+ *   - `stream` is a hipStream_t (the caller's current stream), passed as void*.
+ *   - per-batch scalars (`*_host` arrays, <= QIE_MAX_BATCH entries) are read on
+ *     the host at launch time and passed to the kernel by value.
+ *   - return 0 on success, QIE_ERR_* (< 0) on a rejected argument, or a
+ *     positive hipError_t when the launch itself failed.
+ *   - re-entrant; one caller thread per process (server.py:39 single worker).
+ */
+#ifndef QIE_H_
+#define QIE_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define QIE_ABI_VERSION 1
+#define QIE_MAX_BATCH 16
+
+#define QIE_OK 0
+#define QIE_ERR_INVALID (-1)     /* bad shape / stride / alignment / null pointer */
+#define QIE_ERR_UNSUPPORTED (-2) /* valid but not implemented for these sizes */
+
+#define QIE_ACT_NONE 0
+#define QIE_ACT_GELU_TANH 1
+
+typedef void* qie_stream_t; /* hipStream_t */
+
+int qie_abi_version(void);
+const char* qie_strerror(int code);
+
+/* ------------------------------------------------------------------ linears
+ * All linears compute y = x[M,K] . W[N,K]^T + bias[N] with bf16 operands, fp32
+ * MFMA accumulation and one rounding of (acc + bias) to bf16 (nn.Linear in
+ * bf16).  K % 64 == 0, N % 4 == 0, 16-byte aligned rows.
+ */
+
+/* K1/K3/K9/K11 -- nn.Linear (+ FeedForward GELU(approximate="tanh")) [U]:
+ * attn.to_q/k/v, add_*_proj, img_mlp.net.0.proj (act=GELU), img_in, txt_in,
+ * proj_out.  y = act(bf16(acc + bias)) -> bf16. */
+int qie_linear_bf16(const void* x, int64_t ldx, const void* w, const void* bias, void* y,
+                    int64_t ldy, int M, int N, int K, int act, qie_stream_t stream);
+
+/* K2/K4 -- attn.to_out[0] / to_add_out / *_mlp.net.2 followed by the block's
+ * gated residual `hidden = hidden + gate * out` [U] (QwenImageTransformerBlock):
+ * resid[m,n] = bf16(resid + bf16(gate[b(m),n] * bf16(acc + bias))),
+ * b(m) = m / rows_per_batch, gate row stride gate_bstride (elements). */
+int qie_linear_gated_residual_bf16(const void* x, int64_t ldx, const void* w, const void* bias,
+                                   const void* gate, int64_t gate_bstride, int rows_per_batch,
+                                   void* resid, int64_t ldr, int M, int N, int K,
+                                   qie_stream_t stream);
+
+/* K1 fused -- to_q|to_k|to_v (or add_q|k|v_proj) as ONE GEMM over the packed
+ * weight [3*H*Dh, K]; the epilogue scatters bf16(acc + bias) into the
+ * head-major joint buffer qkv[3][batch][heads][s_pad][head_dim] at sequence
+ * position seq_offset + (m % rows_per_batch) of batch m / rows_per_batch
+ * (replaces the projections + unflatten + torch.cat of
+ * QwenDoubleStreamAttnProcessor2_0 [U]). */
+int qie_linear_qkv_bf16(const void* x, int64_t ldx, const void* w, const void* bias, void* qkv,
+                        int M, int K, int rows_per_batch, int seq_offset, int batch, int heads,
+                        int head_dim, int s_pad, qie_stream_t stream);
+
+/* K5/K10 -- skinny linear for M <= 16 rows (img_mod/txt_mod Linear(3072->18432)
+ * on SiLU(temb), timestep_embedder linears, norm_out.linear) [U]:
+ * weight-bandwidth bound, y = bf16(acc + bias). */
+int qie_gemv_bf16(const void* x, int64_t ldx, const void* w, const void* bias, void* y,
+                  int64_t ldy, int M, int N, int K, qie_stream_t stream);
+
+/* ------------------------------------------------------------------ norms */
+
+/* K6 -- nn.LayerNorm(elementwise_affine=False, eps) + _modulate [U]:
+ * y = bf16(bf16(bf16(LN(x)) * bf16(1 + scale[b])) + shift[b]), fp32 statistics.
+ * shift/scale rows are mod_bstride elements apart per batch. */
+int qie_layernorm_modulate_bf16(const void* x, int64_t ldx, const void* shift, const void* scale,
+                                int64_t mod_bstride, int rows_per_batch, void* y, int64_t ldy,
+                                int rows, int D, float eps, qie_stream_t stream);
+
+/* K9 -- RMSNorm(D, eps, elementwise_affine=True) [U] (txt_norm):
+ * y = bf16(bf16(x * rsqrt(mean(x^2) + eps)) * w). */
+int qie_rmsnorm_bf16(const void* x, const void* w, void* y, int rows, int D, float eps,
+                     qie_stream_t stream);
+
+/* K7 -- attn.norm_q/norm_k (or norm_added_q/k) RMSNorm(head_dim) followed by
+ * apply_rotary_emb_qwen(use_real=False) [U], in place on sequence rows
+ * [seg_start, seg_start + seg_len) of the Q and K planes of the joint buffer.
+ * cos_tab/sin_tab: fp32 [seg_len][head_dim/2] rows for that segment. */
+int qie_qk_norm_rope_bf16(void* qkv, int batch, int heads, int head_dim, int s_pad, int seg_start,
+                          int seg_len, const void* wq, const void* wk, const float* cos_tab,
+                          const float* sin_tab, float eps, qie_stream_t stream);
+
+/* ------------------------------------------------------------------ attention */
+
+/* K8 -- joint non-causal SDPA of QwenDoubleStreamAttnProcessor2_0 [U] over the
+ * head-major joint buffer (head_dim 128).  Keys j >= kv_len_host[b] are masked
+ * (batched CFG text padding).  Query row s of batch b is written to
+ * out_img[(b*s_img + s)*heads*128 + h*128 + d] for s < s_img and to
+ * out_txt[(b*txt_rows + s - s_img)*...] for s_img <= s < s_img + txt_rows.
+ * s_pad % 256 == 0.  scale = 1/sqrt(head_dim) in the reference. */
+int qie_attention_fwd_bf16(const void* qkv, int batch, int heads, int s_pad,
+                           const int* kv_len_host, void* out_img, void* out_txt, int s_img,
+                           int txt_rows, float scale, qie_stream_t stream);
+
+/* ------------------------------------------------------------------ small ops */
+
+/* K10 -- Timesteps(dim, flip_sin_to_cos=True, downscale_freq_shift=0,
+ * scale=1000) [U]: t bf16 [batch] -> bf16 [batch, dim] = [cos | sin]. */
+int qie_timestep_embed_bf16(const void* t, void* out, int batch, int dim, qie_stream_t stream);
+
+/* nn.SiLU on a bf16 vector (temb -> SiLU(temb) feeding every *_mod Linear). */
+int qie_silu_bf16(const void* x, void* y, int64_t n, qie_stream_t stream);
+
+/* K12a -- true-CFG combine + per-token norm rescale of the Edit-Plus pipeline
+ * [U]: comb = u + s*(c-u); out = comb*(|c|/|comb|), all bf16
+ * tensor ops, norms over the last dim C (fp32 accumulate).  Each of the `batch`
+ * slices is [rows][C] contiguous; slices are *_bstride elements apart. */
+int qie_cfg_combine_bf16(const void* cond, int64_t cond_bstride, const void* uncond,
+                         int64_t uncond_bstride, void* out, int64_t out_bstride, int batch, int rows,
+                         int C, float scale, qie_stream_t stream);
+
+/* K12b -- FlowMatchEulerDiscreteScheduler.step [U] with per-batch-row dt
+ * (stream batch: each row at its own sigma): out = bf16(x + bf16(dt[b] * v)).
+ * Tensors are [batch][n] with independent batch strides (elements). */
+int qie_euler_step_bf16(const void* x, int64_t x_bstride, const void* v, int64_t v_bstride,
+                        void* out, int64_t out_bstride, int batch, int64_t n,
+                        const float* dt_host, qie_stream_t stream);
+
+/* strided batch copy of bf16 rows (latents / cond latents into the model input) */
+int qie_copy_bf16(const void* src, int64_t src_bstride, void* dst, int64_t dst_bstride, int batch,
+                  int64_t n, qie_stream_t stream);
+
+/* a5 -- _pack_latents / _unpack_latents [U]: [B,C,H,W] <-> [B,(H/2)(W/2),4C]. */
+int qie_pack_latents_bf16(const void* x, void* y, int batch, int C, int H, int W,
+                          qie_stream_t stream);
+int qie_unpack_latents_bf16(const void* x, void* y, int batch, int C, int H, int W,
+                            qie_stream_t stream);
+
+/* ------------------------------------------------------------------ int8 (a16)
+ * Int8Linear (README.md:136-141, absent from the snapshot; bnb LLM.int8 at
+ * benchmark_int8.py:72-76 is the reference's int8 semantics): W8A8 with
+ * per-output-channel weight scales and per-token dynamic activation scales,
+ * i8 MFMA with int32 accumulation, fp32 dequant epilogue (oracle/int8_ref.py). */
+
+/* per-row symmetric quantisation: q = clamp(rint(x*127/amax)), scale = amax/127 */
+int qie_quantize_rows_i8(const void* x, int64_t ldx, void* q, int64_t ldq, float* scale, int rows,
+                         int D, qie_stream_t stream);
+
+/* K6 + quantisation prologue fused: LayerNorm+modulate as above, emitted as
+ * int8 rows + fp32 per-row scales (the bf16 value is quantised). */
+int qie_layernorm_modulate_i8(const void* x, int64_t ldx, const void* shift, const void* scale,
+                              int64_t mod_bstride, int rows_per_batch, void* q, int64_t ldq,
+                              float* qscale, int rows, int D, float eps, qie_stream_t stream);
+
+/* int8 linears: y = epilogue(bf16(fma(float(acc), sx[m]*sw[n], bias[n]))),
+ * K % 128 == 0; same epilogues as the bf16 family. */
+int qie_linear_i8(const void* xq, int64_t ldx, const float* sx, const void* wq, const float* sw,
+                  const void* bias, void* y, int64_t ldy, int M, int N, int K, int act,
+                  qie_stream_t stream);
+int qie_linear_gated_residual_i8(const void* xq, int64_t ldx, const float* sx, const void* wq,
+                                 const float* sw, const void* bias, const void* gate,
+                                 int64_t gate_bstride, int rows_per_batch, void* resid,
+                                 int64_t ldr, int M, int N, int K, qie_stream_t stream);
+int qie_linear_qkv_i8(const void* xq, int64_t ldx, const float* sx, const void* wq,
+                      const float* sw, const void* bias, void* qkv, int M, int K,
+                      int rows_per_batch, int seq_offset, int batch, int heads, int head_dim,
+                      int s_pad, qie_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* QIE_H_ */

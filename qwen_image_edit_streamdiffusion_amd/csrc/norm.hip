@@ -1,0 +1,275 @@
+// Row-wise normalisation kernels (HBM-bound; one wave per row, 16-byte lanes).
+//
+//  * LayerNorm(no affine) + AdaLN _modulate of QwenImageTransformerBlock [U]
+//    (SURVEY.md §2D K6, §8 a9), optionally emitting int8 + per-row scale for
+//    the Int8Linear path (a16: the quantisation prologue fused into the norm);
+//  * RMSNorm with weight (txt_norm, K9);
+//  * per-head RMSNorm(128) of q/k + complex RoPE (K7, §8 a11), in place on the
+//    head-major joint QKV buffer;
+//  * per-row int8 quantisation of GEMM inputs that are not produced by a norm
+//    (attention output, GELU output).
+// Every elementwise op mirrors the bf16 rounding points of the reference model
+// (oracle/dit_ref.py); statistics are fp32.
+#include "qie_common.h"
+
+namespace {
+
+constexpr int kMaxC = 8;  // 16-byte chunks per lane: D <= 64*8*8 = 4096
+
+__device__ __forceinline__ void unpack8(const u32x4_t w, float f[8]) {
+  f[0] = lo_f(w.x); f[1] = hi_f(w.x); f[2] = lo_f(w.y); f[3] = hi_f(w.y);
+  f[4] = lo_f(w.z); f[5] = hi_f(w.z); f[6] = lo_f(w.w); f[7] = hi_f(w.w);
+}
+__device__ __forceinline__ u32x4_t pack8(const float f[8]) {
+  return u32x4_t{pack2(f[0], f[1]), pack2(f[2], f[3]), pack2(f[4], f[5]), pack2(f[6], f[7])};
+}
+
+// symmetric int8 of 8 values with a precomputed inverse scale; returns 8 bytes
+__device__ __forceinline__ u32x2_t quant8(const float f[8], float inv) {
+  unsigned w[2] = {0, 0};
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    float q = rintf(f[j] * inv);
+    q = fminf(fmaxf(q, -127.f), 127.f);
+    w[j >> 2] |= ((unsigned)((int)q & 0xff)) << (8 * (j & 3));
+  }
+  return u32x2_t{w[0], w[1]};
+}
+
+template <bool I8>
+__global__ void __launch_bounds__(256)
+    ln_mod_kernel(const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __restrict__ shift,
+                  const bf16_t* __restrict__ scale, int64_t mod_bstride, int rpb, void* y, int64_t ldy,
+                  float* qscale, int rows, int D, float eps) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int lane = threadIdx.x & 63;
+  const int nch = D >> 3;
+  const bf16_t* xr = x + (int64_t)row * ldx;
+  float v[kMaxC][8];
+  float sum = 0.f;
+#pragma unroll
+  for (int i = 0; i < kMaxC; ++i) {
+    const int c = lane + 64 * i;
+    if (c < nch) {
+      unpack8(*(const u32x4_t*)(xr + c * 8), v[i]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sum += v[i][j];
+    }
+  }
+  const float mean = wave_sum(sum) / (float)D;
+  float sq = 0.f;
+#pragma unroll
+  for (int i = 0; i < kMaxC; ++i)
+    if (lane + 64 * i < nch)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d = v[i][j] - mean;
+        sq += d * d;
+      }
+  const float rstd = rsqrtf(wave_sum(sq) / (float)D + eps);
+  const int b = row / rpb;
+  const bf16_t* sh = shift + (int64_t)b * mod_bstride;
+  const bf16_t* sc = scale + (int64_t)b * mod_bstride;
+  float amax = 0.f;
+#pragma unroll
+  for (int i = 0; i < kMaxC; ++i) {
+    const int c = lane + 64 * i;
+    if (c < nch) {
+      float s8[8], h8[8];
+      unpack8(*(const u32x4_t*)(sc + c * 8), s8);
+      unpack8(*(const u32x4_t*)(sh + c * 8), h8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float n = rbf((v[i][j] - mean) * rstd);
+        const float t = rbf(n * rbf(1.0f + s8[j]));
+        v[i][j] = rbf(t + h8[j]);
+        amax = fmaxf(amax, fabsf(v[i][j]));
+      }
+      if constexpr (!I8) *(u32x4_t*)((bf16_t*)y + (int64_t)row * ldy + c * 8) = pack8(v[i]);
+    }
+  }
+  if constexpr (I8) {
+    amax = wave_max(amax);
+    const float inv = amax > 0.f ? 127.0f / amax : 0.f;
+    int8_t* qr = (int8_t*)y + (int64_t)row * ldy;
+#pragma unroll
+    for (int i = 0; i < kMaxC; ++i) {
+      const int c = lane + 64 * i;
+      if (c < nch) *(u32x2_t*)(qr + c * 8) = quant8(v[i], inv);
+    }
+    if (lane == 0) qscale[row] = amax > 0.f ? amax / 127.0f : 1.0f;
+  }
+}
+
+__global__ void __launch_bounds__(256)
+    rmsnorm_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16_t* __restrict__ y,
+                   int rows, int D, float eps) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int lane = threadIdx.x & 63;
+  const int nch = D >> 3;
+  const bf16_t* xr = x + (int64_t)row * D;
+  float v[kMaxC][8];
+  float sq = 0.f;
+#pragma unroll
+  for (int i = 0; i < kMaxC; ++i) {
+    const int c = lane + 64 * i;
+    if (c < nch) {
+      unpack8(*(const u32x4_t*)(xr + c * 8), v[i]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sq += v[i][j] * v[i][j];
+    }
+  }
+  const float rstd = rsqrtf(wave_sum(sq) / (float)D + eps);
+#pragma unroll
+  for (int i = 0; i < kMaxC; ++i) {
+    const int c = lane + 64 * i;
+    if (c < nch) {
+      float w8[8];
+      unpack8(*(const u32x4_t*)(w + c * 8), w8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[i][j] = rbf(rbf(v[i][j] * rstd) * w8[j]);
+      *(u32x4_t*)(y + (int64_t)row * D + c * 8) = pack8(v[i]);
+    }
+  }
+}
+
+// 16 lanes per 128-wide head row, 8 elements (4 complex pairs) per lane.
+__global__ void __launch_bounds__(256)
+    qk_norm_rope_kernel(bf16_t* __restrict__ qkv, int B, int H, int s_pad, int seg_start, int seg_len,
+                        const bf16_t* __restrict__ wq, const bf16_t* __restrict__ wk,
+                        const float* __restrict__ cos_tab, const float* __restrict__ sin_tab,
+                        float eps) {
+  const int64_t gr = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4);  // global row id
+  const int64_t total = (int64_t)2 * B * H * seg_len;
+  if (gr >= total) return;
+  const int l16 = threadIdx.x & 15;
+  const int sl = (int)(gr % seg_len);
+  const int64_t plane = gr / seg_len;  // (which*B + b)*H + h, which in {0,1}
+  const int which = (int)(plane / ((int64_t)B * H));
+  bf16_t* p = qkv + (plane * s_pad + seg_start + sl) * 128 + l16 * 8;
+  float v[8];
+  unpack8(*(const u32x4_t*)p, v);
+  float sq = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) sq += v[j] * v[j];
+  sq = group_sum<16>(sq);
+  const float rstd = rsqrtf(sq * (1.0f / 128.0f) + eps);
+  float w8[8];
+  unpack8(*(const u32x4_t*)((which == 0 ? wq : wk) + l16 * 8), w8);
+  const f32x4_t cs = *(const f32x4_t*)(cos_tab + (int64_t)sl * 64 + l16 * 4);
+  const f32x4_t sn = *(const f32x4_t*)(sin_tab + (int64_t)sl * 64 + l16 * 4);
+  float o[8];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float a = rbf(rbf(v[2 * j] * rstd) * w8[2 * j]);
+    const float bb = rbf(rbf(v[2 * j + 1] * rstd) * w8[2 * j + 1]);
+    o[2 * j] = a * cs[j] - bb * sn[j];
+    o[2 * j + 1] = a * sn[j] + bb * cs[j];
+  }
+  *(u32x4_t*)p = pack8(o);
+}
+
+template <int MAXC>
+__global__ void __launch_bounds__(256)
+    quant_rows_kernel(const bf16_t* __restrict__ x, int64_t ldx, int8_t* __restrict__ q, int64_t ldq,
+                      float* __restrict__ scale, int rows, int D) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int lane = threadIdx.x & 63;
+  const int nch = D >> 3;
+  const bf16_t* xr = x + (int64_t)row * ldx;
+  u32x4_t raw[MAXC];
+  float amax = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXC; ++i) {
+    const int c = lane + 64 * i;
+    if (c < nch) {
+      raw[i] = *(const u32x4_t*)(xr + c * 8);
+      float f[8];
+      unpack8(raw[i], f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf(f[j]));
+    }
+  }
+  amax = wave_max(amax);
+  const float inv = amax > 0.f ? 127.0f / amax : 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXC; ++i) {
+    const int c = lane + 64 * i;
+    if (c < nch) {
+      float f[8];
+      unpack8(raw[i], f);
+      *(u32x2_t*)(q + (int64_t)row * ldq + c * 8) = quant8(f, inv);
+    }
+  }
+  if (lane == 0) scale[row] = amax > 0.f ? amax / 127.0f : 1.0f;
+}
+
+}  // namespace
+
+extern "C" int qie_layernorm_modulate_bf16(const void* x, int64_t ldx, const void* shift,
+                                           const void* scale, int64_t mod_bstride,
+                                           int rows_per_batch, void* y, int64_t ldy, int rows, int D,
+                                           float eps, qie_stream_t stream) {
+  QIE_CHECK_ARG(x && shift && scale && y && rows > 0 && rows_per_batch > 0);
+  QIE_CHECK_ARG(D % 8 == 0 && D <= 64 * 8 * kMaxC && ldx % 8 == 0 && ldy % 8 == 0);
+  QIE_CHECK_ARG(mod_bstride % 8 == 0);
+  ln_mod_kernel<false><<<(rows + 3) / 4, 256, 0, (hipStream_t)stream>>>(
+      (const bf16_t*)x, ldx, (const bf16_t*)shift, (const bf16_t*)scale, mod_bstride, rows_per_batch,
+      y, ldy, nullptr, rows, D, eps);
+  return qie_last_error();
+}
+
+extern "C" int qie_layernorm_modulate_i8(const void* x, int64_t ldx, const void* shift,
+                                         const void* scale, int64_t mod_bstride,
+                                         int rows_per_batch, void* q, int64_t ldq, float* qscale,
+                                         int rows, int D, float eps, qie_stream_t stream) {
+  QIE_CHECK_ARG(x && shift && scale && q && qscale && rows > 0 && rows_per_batch > 0);
+  QIE_CHECK_ARG(D % 8 == 0 && D <= 64 * 8 * kMaxC && ldx % 8 == 0 && ldq % 8 == 0);
+  QIE_CHECK_ARG(mod_bstride % 8 == 0);
+  ln_mod_kernel<true><<<(rows + 3) / 4, 256, 0, (hipStream_t)stream>>>(
+      (const bf16_t*)x, ldx, (const bf16_t*)shift, (const bf16_t*)scale, mod_bstride, rows_per_batch,
+      q, ldq, qscale, rows, D, eps);
+  return qie_last_error();
+}
+
+extern "C" int qie_rmsnorm_bf16(const void* x, const void* w, void* y, int rows, int D, float eps,
+                                qie_stream_t stream) {
+  QIE_CHECK_ARG(x && w && y && rows > 0 && D % 8 == 0 && D <= 64 * 8 * kMaxC);
+  rmsnorm_kernel<<<(rows + 3) / 4, 256, 0, (hipStream_t)stream>>>(
+      (const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y, rows, D, eps);
+  return qie_last_error();
+}
+
+extern "C" int qie_qk_norm_rope_bf16(void* qkv, int batch, int heads, int head_dim, int s_pad,
+                                     int seg_start, int seg_len, const void* wq, const void* wk,
+                                     const float* cos_tab, const float* sin_tab, float eps,
+                                     qie_stream_t stream) {
+  QIE_CHECK_ARG(qkv && wq && wk && cos_tab && sin_tab && head_dim == 128);
+  QIE_CHECK_ARG(batch > 0 && heads > 0 && seg_len >= 0 && seg_start >= 0 &&
+                seg_start + seg_len <= s_pad);
+  if (seg_len == 0) return QIE_OK;
+  const int64_t rows = (int64_t)2 * batch * heads * seg_len;
+  const int64_t blocks = (rows + 15) / 16;
+  QIE_CHECK_ARG(blocks < (1ll << 31));
+  qk_norm_rope_kernel<<<(unsigned)blocks, 256, 0, (hipStream_t)stream>>>(
+      (bf16_t*)qkv, batch, heads, s_pad, seg_start, seg_len, (const bf16_t*)wq, (const bf16_t*)wk,
+      cos_tab, sin_tab, eps);
+  return qie_last_error();
+}
+
+extern "C" int qie_quantize_rows_i8(const void* x, int64_t ldx, void* q, int64_t ldq, float* scale,
+                                    int rows, int D, qie_stream_t stream) {
+  QIE_CHECK_ARG(x && q && scale && rows > 0 && D % 8 == 0 && ldx % 8 == 0 && ldq % 8 == 0);
+  hipStream_t s = (hipStream_t)stream;
+  const int grid = (rows + 3) / 4;
+  if (D <= 64 * 8 * 8)
+    quant_rows_kernel<8><<<grid, 256, 0, s>>>((const bf16_t*)x, ldx, (int8_t*)q, ldq, scale, rows, D);
+  else if (D <= 64 * 8 * 24)
+    quant_rows_kernel<24><<<grid, 256, 0, s>>>((const bf16_t*)x, ldx, (int8_t*)q, ldq, scale, rows, D);
+  else
+    return QIE_ERR_UNSUPPORTED;
+  return qie_last_error();
+}

@@ -1,0 +1,294 @@
+"""Tensor-level wrappers over the libqie C ABI (include/qie.h).
+
+Every function validates shapes/dtypes/strides on the host before launching
+(a bad launch on a shared GPU box is expensive), launches on the caller's
+current HIP stream and raises ``QieError`` on any failure.  PyTorch only
+provides device memory and the stream here.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+from typing import Optional, Sequence
+
+import torch
+
+from . import _lib
+
+BF16 = torch.bfloat16
+ACT_NONE, ACT_GELU = 0, 1
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _p(t: Optional[torch.Tensor]) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+def _chk(cond: bool, msg: str):
+    if not cond:
+        raise ValueError(msg)
+
+
+def _is2d_rowmajor(t: torch.Tensor) -> bool:
+    return t.dim() == 2 and t.stride(1) == 1
+
+
+def _dev(*ts):
+    for t in ts:
+        if t is not None:
+            _chk(t.is_cuda, "libqie ops need device tensors")
+
+
+# ---------------------------------------------------------------------------- linears
+def linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None,
+           act: int = ACT_NONE) -> torch.Tensor:
+    """y = act(bf16(x @ w.T + b)); x [M,K] (row stride may exceed K), w [N,K]."""
+    _dev(x, w, b)
+    _chk(x.dtype == BF16 and w.dtype == BF16 and b.dtype == BF16, "bf16 operands required")
+    _chk(_is2d_rowmajor(x) and w.is_contiguous() and b.is_contiguous(), "row-major operands")
+    M, K = x.shape
+    N = w.shape[0]
+    _chk(w.shape[1] == K and b.numel() == N, f"shape mismatch x{tuple(x.shape)} w{tuple(w.shape)}")
+    _chk(K % 64 == 0 and N % 4 == 0, "K % 64 == 0 and N % 4 == 0 required")
+    if out is None:
+        out = torch.empty(M, N, dtype=BF16, device=x.device)
+    _chk(_is2d_rowmajor(out) and out.shape == (M, N) and out.dtype == BF16, "bad out")
+    if M <= 16 and act == ACT_NONE:
+        _lib.call("qie_gemv_bf16", _p(x), x.stride(0), _p(w), _p(b), _p(out), out.stride(0), M, N, K,
+                  _stream())
+    else:
+        _lib.call("qie_linear_bf16", _p(x), x.stride(0), _p(w), _p(b), _p(out), out.stride(0), M, N,
+                  K, act, _stream())
+    return out
+
+
+def gemv(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None):
+    """Skinny linear for M <= 16 (modulation / timestep linears)."""
+    _dev(x, w, b)
+    M, K = x.shape
+    N = w.shape[0]
+    _chk(M <= 16 and w.shape[1] == K and K % 8 == 0 and _is2d_rowmajor(x), "gemv shapes")
+    if out is None:
+        out = torch.empty(M, N, dtype=BF16, device=x.device)
+    _lib.call("qie_gemv_bf16", _p(x), x.stride(0), _p(w), _p(b), _p(out), out.stride(0), M, N, K,
+              _stream())
+    return out
+
+
+def linear_gated_residual(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, gate: torch.Tensor,
+                          rows_per_batch: int, resid: torch.Tensor) -> torch.Tensor:
+    """resid += gate[b(m)] * (x @ w.T + b) with the reference's bf16 rounding."""
+    _dev(x, w, b, gate, resid)
+    M, K = x.shape
+    N = w.shape[0]
+    _chk(_is2d_rowmajor(x) and w.shape[1] == K and resid.shape == (M, N), "gated residual shapes")
+    _chk(gate.dim() == 2 and gate.stride(1) == 1 and gate.shape[1] >= N, "gate [B, >=N]")
+    _chk(M % rows_per_batch == 0 and gate.shape[0] >= M // rows_per_batch, "gate batch")
+    _chk(K % 64 == 0 and N % 4 == 0, "K % 64, N % 4")
+    _lib.call("qie_linear_gated_residual_bf16", _p(x), x.stride(0), _p(w), _p(b), _p(gate),
+              gate.stride(0), rows_per_batch, _p(resid), resid.stride(0), M, N, K, _stream())
+    return resid
+
+
+def linear_qkv(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, qkv: torch.Tensor,
+               rows_per_batch: int, seq_offset: int) -> None:
+    """Fused q|k|v projection scattered into qkv [3, B, H, S_pad, Dh]."""
+    _dev(x, w, b, qkv)
+    M, K = x.shape
+    _, B, H, S_pad, Dh = qkv.shape
+    _chk(qkv.is_contiguous() and w.shape == (3 * H * Dh, K) and b.numel() == 3 * H * Dh, "qkv shapes")
+    _chk(M == B * rows_per_batch and seq_offset + rows_per_batch <= S_pad, "qkv rows")
+    _chk(K % 64 == 0 and _is2d_rowmajor(x), "qkv K")
+    _lib.call("qie_linear_qkv_bf16", _p(x), x.stride(0), _p(w), _p(b), _p(qkv), M, K, rows_per_batch,
+              seq_offset, B, H, Dh, S_pad, _stream())
+
+
+# ---------------------------------------------------------------------------- norms
+def layernorm_modulate(x: torch.Tensor, shift: torch.Tensor, scale: torch.Tensor, rows_per_batch: int,
+                       out: Optional[torch.Tensor] = None, eps: float = 1e-6) -> torch.Tensor:
+    """bf16(LN(x) * (1 + scale[b]) + shift[b]); shift/scale: [B, D] views (row stride any)."""
+    _dev(x, shift, scale)
+    R, D = x.shape
+    _chk(_is2d_rowmajor(x) and shift.stride(1) == 1 and scale.stride(1) == 1, "ln rows")
+    _chk(shift.stride(0) == scale.stride(0), "shift/scale must share a batch stride")
+    _chk(R % rows_per_batch == 0 and shift.shape[0] >= R // rows_per_batch and D % 8 == 0, "ln shapes")
+    if out is None:
+        out = torch.empty(R, D, dtype=BF16, device=x.device)
+    _lib.call("qie_layernorm_modulate_bf16", _p(x), x.stride(0), _p(shift), _p(scale), shift.stride(0),
+              rows_per_batch, _p(out), out.stride(0), R, D, eps, _stream())
+    return out
+
+
+def layernorm_modulate_i8(x, shift, scale, rows_per_batch: int, q: torch.Tensor, qscale: torch.Tensor,
+                          eps: float = 1e-6):
+    _dev(x, shift, scale, q, qscale)
+    R, D = x.shape
+    _chk(q.dtype == torch.int8 and q.shape == (R, D) and qscale.dtype == torch.float32, "i8 out")
+    _chk(shift.stride(0) == scale.stride(0) and R % rows_per_batch == 0, "ln i8")
+    _lib.call("qie_layernorm_modulate_i8", _p(x), x.stride(0), _p(shift), _p(scale), shift.stride(0),
+              rows_per_batch, _p(q), q.stride(0), _p(qscale), R, D, eps, _stream())
+
+
+def rmsnorm(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None, eps: float = 1e-6):
+    _dev(x, w)
+    R, D = x.shape
+    _chk(x.is_contiguous() and w.numel() == D and D % 8 == 0 and D <= 4096, "rmsnorm shapes")
+    if out is None:
+        out = torch.empty_like(x)
+    _lib.call("qie_rmsnorm_bf16", _p(x), _p(w), _p(out), R, D, eps, _stream())
+    return out
+
+
+def qk_norm_rope(qkv: torch.Tensor, seg_start: int, seg_len: int, wq: torch.Tensor, wk: torch.Tensor,
+                 cos_tab: torch.Tensor, sin_tab: torch.Tensor, eps: float = 1e-6):
+    _dev(qkv, wq, wk, cos_tab, sin_tab)
+    _, B, H, S_pad, Dh = qkv.shape
+    _chk(Dh == 128 and seg_start + seg_len <= S_pad, "qk_norm_rope segment")
+    _chk(cos_tab.dtype == torch.float32 and cos_tab.shape[0] >= seg_len and cos_tab.shape[1] == 64,
+         "rope table [seg_len, 64] fp32")
+    _chk(cos_tab.is_contiguous() and sin_tab.is_contiguous() and sin_tab.shape == cos_tab.shape, "rope")
+    _lib.call("qie_qk_norm_rope_bf16", _p(qkv), B, H, Dh, S_pad, seg_start, seg_len, _p(wq), _p(wk),
+              _p(cos_tab), _p(sin_tab), eps, _stream())
+
+
+def quantize_rows(x: torch.Tensor, q: torch.Tensor, scale: torch.Tensor):
+    _dev(x, q, scale)
+    R, D = x.shape
+    _chk(q.shape == (R, D) and q.dtype == torch.int8 and scale.numel() >= R, "quantize shapes")
+    _lib.call("qie_quantize_rows_i8", _p(x), x.stride(0), _p(q), q.stride(0), _p(scale), R, D, _stream())
+
+
+# ---------------------------------------------------------------------------- attention
+def attention(qkv: torch.Tensor, kv_len: Sequence[int], out_img: torch.Tensor,
+              out_txt: Optional[torch.Tensor], s_img: int, txt_rows: int,
+              scale: Optional[float] = None) -> None:
+    _dev(qkv, out_img, out_txt)
+    _, B, H, S_pad, Dh = qkv.shape
+    _chk(Dh == 128 and S_pad % 256 == 0 and len(kv_len) == B and B <= 16, "attention shapes")
+    _chk(out_img.shape == (B * s_img, H * Dh) and out_img.is_contiguous(), "out_img")
+    if txt_rows:
+        _chk(out_txt is not None and out_txt.shape == (B * txt_rows, H * Dh), "out_txt")
+    _chk(all(0 < k <= S_pad for k in kv_len), "kv_len")
+    arr = (ctypes.c_int * B)(*[int(k) for k in kv_len])
+    sc = 1.0 / math.sqrt(Dh) if scale is None else scale
+    _lib.call("qie_attention_fwd_bf16", _p(qkv), B, H, S_pad, arr, _p(out_img), _p(out_txt), s_img,
+              txt_rows, sc, _stream())
+
+
+# ---------------------------------------------------------------------------- small ops
+def timestep_embed(t: torch.Tensor, dim: int = 256, out: Optional[torch.Tensor] = None):
+    _dev(t)
+    _chk(t.dtype == BF16 and t.dim() == 1 and t.is_contiguous(), "t: bf16 [B]")
+    if out is None:
+        out = torch.empty(t.numel(), dim, dtype=BF16, device=t.device)
+    _lib.call("qie_timestep_embed_bf16", _p(t), _p(out), t.numel(), dim, _stream())
+    return out
+
+
+def silu(x: torch.Tensor, out: Optional[torch.Tensor] = None):
+    _dev(x)
+    _chk(x.is_contiguous() and x.dtype == BF16, "silu")
+    if out is None:
+        out = torch.empty_like(x)
+    _lib.call("qie_silu_bf16", _p(x), _p(out), x.numel(), _stream())
+    return out
+
+
+def cfg_combine(cond: torch.Tensor, uncond: torch.Tensor, scale: float,
+                out: Optional[torch.Tensor] = None):
+    """True-CFG combine + norm rescale over [B, rows, C] views whose per-batch
+    slices are contiguous (e.g. ``out[:, :S_noise]`` of a model output)."""
+    _dev(cond, uncond, out)
+    _chk(cond.shape == uncond.shape and cond.dim() == 3, "cfg: [B, rows, C] views")
+    B, rows, C = cond.shape
+    for t in (cond, uncond):
+        _chk(t.stride(2) == 1 and t.stride(1) == C, "cfg: contiguous per-batch slices")
+    if out is None:
+        out = torch.empty(B, rows, C, dtype=BF16, device=cond.device)
+    _chk(out.shape == cond.shape and out.stride(2) == 1 and out.stride(1) == C, "cfg out")
+    _lib.call("qie_cfg_combine_bf16", _p(cond), cond.stride(0), _p(uncond), uncond.stride(0), _p(out),
+              out.stride(0), B, rows, C, float(scale), _stream())
+    return out
+
+
+def euler_step(x: torch.Tensor, v: torch.Tensor, dt: Sequence[float], out: torch.Tensor):
+    """out[b] = bf16(x[b] + bf16(dt[b] * v[b])) for 2-D/3-D [B, ...] views whose
+    per-batch slices are contiguous."""
+    _dev(x, v, out)
+    B = x.shape[0]
+    n = x[0].numel()
+    for t in (x, v, out):
+        _chk(t.shape[0] == B and t[0].is_contiguous() and t[0].numel() == n, "euler shapes")
+    _chk(len(dt) == B and B <= 16, "dt per batch row")
+    arr = (ctypes.c_float * B)(*[float(d) for d in dt])
+    _lib.call("qie_euler_step_bf16", _p(x), x.stride(0), _p(v), v.stride(0), _p(out), out.stride(0), B,
+              n, arr, _stream())
+    return out
+
+
+def copy_batched(src: torch.Tensor, dst: torch.Tensor):
+    """dst[b] = src[b] for [B, ...] views with contiguous per-batch slices."""
+    _dev(src, dst)
+    B = src.shape[0]
+    n = src[0].numel()
+    _chk(dst.shape[0] == B and dst[0].numel() == n and src[0].is_contiguous() and dst[0].is_contiguous(),
+         "copy shapes")
+    _lib.call("qie_copy_bf16", _p(src), src.stride(0), _p(dst), dst.stride(0), B, n, _stream())
+    return dst
+
+
+def pack_latents(x: torch.Tensor) -> torch.Tensor:
+    """[B, C, H, W] (or [B, C, 1, H, W]) -> [B, (H/2)(W/2), 4C] (diffusers _pack_latents)."""
+    _dev(x)
+    if x.dim() == 5:
+        x = x[:, :, 0]
+    x = x.contiguous()
+    B, C, H, W = x.shape
+    y = torch.empty(B, (H // 2) * (W // 2), 4 * C, dtype=BF16, device=x.device)
+    _lib.call("qie_pack_latents_bf16", _p(x), _p(y), B, C, H, W, _stream())
+    return y
+
+
+def unpack_latents(x: torch.Tensor, H: int, W: int) -> torch.Tensor:
+    """[B, (H/2)(W/2), 4C] -> [B, C, 1, H, W] (H, W in latent pixels)."""
+    _dev(x)
+    x = x.contiguous()
+    B, N, C4 = x.shape
+    C = C4 // 4
+    _chk(N == (H // 2) * (W // 2), "unpack shape")
+    y = torch.empty(B, C, 1, H, W, dtype=BF16, device=x.device)
+    _lib.call("qie_unpack_latents_bf16", _p(x), _p(y), B, C, H, W, _stream())
+    return y
+
+
+# ---------------------------------------------------------------------------- int8 linears
+def linear_i8(xq, sx, wq, sw, b, out, act: int = ACT_NONE):
+    M, K = xq.shape
+    N = wq.shape[0]
+    _chk(xq.dtype == torch.int8 and wq.dtype == torch.int8 and wq.shape[1] == K and K % 128 == 0, "i8")
+    _chk(out.shape == (M, N) and out.dtype == BF16, "i8 out")
+    _lib.call("qie_linear_i8", _p(xq), xq.stride(0), _p(sx), _p(wq), _p(sw), _p(b), _p(out),
+              out.stride(0), M, N, K, act, _stream())
+    return out
+
+
+def linear_gated_residual_i8(xq, sx, wq, sw, b, gate, rows_per_batch: int, resid):
+    M, K = xq.shape
+    N = wq.shape[0]
+    _chk(xq.dtype == torch.int8 and wq.shape[1] == K and K % 128 == 0 and resid.shape == (M, N), "i8 gr")
+    _chk(M % rows_per_batch == 0 and gate.shape[0] >= M // rows_per_batch, "i8 gate")
+    _lib.call("qie_linear_gated_residual_i8", _p(xq), xq.stride(0), _p(sx), _p(wq), _p(sw), _p(b),
+              _p(gate), gate.stride(0), rows_per_batch, _p(resid), resid.stride(0), M, N, K, _stream())
+    return resid
+
+
+def linear_qkv_i8(xq, sx, wq, sw, b, qkv, rows_per_batch: int, seq_offset: int):
+    M, K = xq.shape
+    _, B, H, S_pad, Dh = qkv.shape
+    _chk(xq.dtype == torch.int8 and wq.shape == (3 * H * Dh, K) and K % 128 == 0, "i8 qkv")
+    _chk(M == B * rows_per_batch and seq_offset + rows_per_batch <= S_pad, "i8 qkv rows")
+    _lib.call("qie_linear_qkv_i8", _p(xq), xq.stride(0), _p(sx), _p(wq), _p(sw), _p(b), _p(qkv), M, K,
+              rows_per_batch, seq_offset, B, H, Dh, S_pad, _stream())

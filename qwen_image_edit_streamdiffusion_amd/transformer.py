@@ -1,0 +1,478 @@
+"""HIP-backed drop-in for diffusers ``QwenImageTransformer2DModel`` [U].
+
+The reference swaps this module in as ``pipeline.transformer = <module>``
+(benchmark_compile.py:102-106, benchmark_lightning_compile.py:89-93,
+test_compiled.py:39-43) and the Edit-Plus pipeline calls it once per denoise
+step per CFG branch (SURVEY.md §3.4, §8 b).  Same constructor config, same
+``forward`` signature and return convention, same diffusers state_dict names
+(``load_state_dict`` / LoRA fuse address them), plus ``.config``, ``.dtype``,
+``.device`` and a no-op ``cache_context``.
+
+Every arithmetic op of the forward runs in libqie.so (include/qie.h); torch
+only owns the HBM buffers and the stream.  Weights are kept packed for the
+kernels: q|k|v fused into one [3D, D] matrix per stream.
+
+HBM layout per forward (B rows, S_img image tokens, S_txt text tokens):
+  x_img [B*S_img, D], x_txt [B*S_txt, D]      residual streams (bf16)
+  h_*                                          LN+modulate outputs
+  qkv   [3][B][H][S_pad][128]                  joint [image; text; pad] sequence
+  att_* [B*S_*, D], mlp_* [B*S_*, 4D]          attention / GELU outputs
+"""
+from __future__ import annotations
+
+import contextlib
+import math
+from dataclasses import asdict, dataclass, field
+from typing import Dict, Iterator, List, Optional, Sequence, Tuple
+
+import torch
+from torch import nn
+
+from . import ops
+from .rope import rope_tables
+
+BF16 = torch.bfloat16
+
+
+@dataclass
+class TransformerConfig:
+    """``QwenImageTransformer2DModel.config`` (SURVEY.md §8 b)."""
+
+    patch_size: int = 2
+    in_channels: int = 64
+    out_channels: int = 16
+    num_layers: int = 60
+    attention_head_dim: int = 128
+    num_attention_heads: int = 24
+    joint_attention_dim: int = 3584
+    guidance_embeds: bool = False
+    axes_dims_rope: Tuple[int, int, int] = (16, 56, 56)
+
+    @property
+    def inner_dim(self) -> int:
+        return self.num_attention_heads * self.attention_head_dim
+
+    def __getitem__(self, k):  # diffusers FrozenDict-style access
+        return getattr(self, k)
+
+    def get(self, k, default=None):
+        return getattr(self, k, default)
+
+
+@dataclass
+class Transformer2DModelOutput:
+    sample: torch.Tensor
+
+
+class _Block(nn.Module):
+    """Packed weights of one QwenImageTransformerBlock."""
+
+    def __init__(self, D: int, Dh: int, F: int, device, dtype=BF16):
+        super().__init__()
+        e = dict(device=device, dtype=dtype)
+        for s in ("img", "txt"):
+            self.register_buffer(f"w_mod_{s}", torch.empty(6 * D, D, **e))
+            self.register_buffer(f"b_mod_{s}", torch.empty(6 * D, **e))
+            self.register_buffer(f"w_qkv_{s}", torch.empty(3 * D, D, **e))
+            self.register_buffer(f"b_qkv_{s}", torch.empty(3 * D, **e))
+            self.register_buffer(f"w_out_{s}", torch.empty(D, D, **e))
+            self.register_buffer(f"b_out_{s}", torch.empty(D, **e))
+            self.register_buffer(f"w_up_{s}", torch.empty(F, D, **e))
+            self.register_buffer(f"b_up_{s}", torch.empty(F, **e))
+            self.register_buffer(f"w_down_{s}", torch.empty(D, F, **e))
+            self.register_buffer(f"b_down_{s}", torch.empty(D, **e))
+        for n in ("norm_q", "norm_k", "norm_added_q", "norm_added_k"):
+            self.register_buffer(n, torch.empty(Dh, **e))
+        self.q8: Dict[str, Tuple[torch.Tensor, torch.Tensor]] = {}
+
+
+class _Workspace:
+    def __init__(self, cfg: TransformerConfig, B: int, S_img: int, S_txt: int, device, int8: bool):
+        D, H, Dh = cfg.inner_dim, cfg.num_attention_heads, cfg.attention_head_dim
+        F = 4 * D
+        self.S_pad = ((S_img + S_txt + 255) // 256) * 256
+        e = dict(device=device, dtype=BF16)
+        R_i, R_t = B * S_img, B * S_txt
+        self.x_img = torch.empty(R_i, D, **e)
+        self.x_txt = torch.empty(max(R_t, 1), D, **e)
+        self.h_img = torch.empty(R_i, D, **e)
+        self.h_txt = torch.empty(max(R_t, 1), D, **e)
+        self.att_img = torch.empty(R_i, D, **e)
+        self.att_txt = torch.empty(max(R_t, 1), D, **e)
+        self.mlp_img = torch.empty(R_i, F, **e)
+        self.mlp_txt = torch.empty(max(R_t, 1), F, **e)
+        self.qkv = torch.zeros(3, B, H, self.S_pad, Dh, **e)  # pad rows stay 0 (finite V)
+        self.txt_norm = torch.empty(max(R_t, 1), cfg.joint_attention_dim, **e)
+        self.tproj = torch.empty(B, 256, **e)
+        self.t_h = torch.empty(B, D, **e)
+        self.t_hs = torch.empty(B, D, **e)
+        self.temb = torch.empty(B, D, **e)
+        self.stemb = torch.empty(B, D, **e)
+        self.mod_img = torch.empty(B, 6 * D, **e)
+        self.mod_txt = torch.empty(B, 6 * D, **e)
+        self.emb_out = torch.empty(B, 2 * D, **e)
+        self.t_bf = torch.empty(B, **e)
+        if int8:
+            i8 = dict(device=device, dtype=torch.int8)
+            f32 = dict(device=device, dtype=torch.float32)
+            self.q_img = torch.empty(R_i, F, **i8)
+            self.q_txt = torch.empty(max(R_t, 1), F, **i8)
+            self.s_img = torch.empty(R_i, **f32)
+            self.s_txt = torch.empty(max(R_t, 1), **f32)
+
+
+class QwenImageTransformer2DModel(nn.Module):
+    """HIP-backed QwenImageTransformer2DModel (diffusers-compatible surface)."""
+
+    def __init__(self, patch_size: int = 2, in_channels: int = 64, out_channels: int = 16,
+                 num_layers: int = 60, attention_head_dim: int = 128, num_attention_heads: int = 24,
+                 joint_attention_dim: int = 3584, guidance_embeds: bool = False,
+                 axes_dims_rope: Tuple[int, int, int] = (16, 56, 56), device="cuda"):
+        super().__init__()
+        self.config = TransformerConfig(patch_size, in_channels, out_channels, num_layers,
+                                        attention_head_dim, num_attention_heads, joint_attention_dim,
+                                        guidance_embeds, tuple(axes_dims_rope))
+        if guidance_embeds:
+            raise NotImplementedError("guidance_embeds=True is not used by Qwen-Image-Edit-2509")
+        if attention_head_dim != 128:
+            raise NotImplementedError("the attention kernel is specialised for head_dim 128")
+        cfg = self.config
+        D, Dh = cfg.inner_dim, cfg.attention_head_dim
+        F = 4 * D
+        P = patch_size * patch_size * out_channels
+        e = dict(device=device, dtype=BF16)
+        self.register_buffer("img_in_w", torch.empty(D, in_channels, **e))
+        self.register_buffer("img_in_b", torch.empty(D, **e))
+        self.register_buffer("txt_norm_w", torch.empty(joint_attention_dim, **e))
+        self.register_buffer("txt_in_w", torch.empty(D, joint_attention_dim, **e))
+        self.register_buffer("txt_in_b", torch.empty(D, **e))
+        self.register_buffer("t_l1_w", torch.empty(D, 256, **e))
+        self.register_buffer("t_l1_b", torch.empty(D, **e))
+        self.register_buffer("t_l2_w", torch.empty(D, D, **e))
+        self.register_buffer("t_l2_b", torch.empty(D, **e))
+        self.register_buffer("norm_out_w", torch.empty(2 * D, D, **e))
+        self.register_buffer("norm_out_b", torch.empty(2 * D, **e))
+        self.register_buffer("proj_out_w", torch.empty(P, D, **e))
+        self.register_buffer("proj_out_b", torch.empty(P, **e))
+        self.transformer_blocks = nn.ModuleList(_Block(D, Dh, F, device) for _ in range(num_layers))
+        self.int8 = False
+        # optional kernel probe: {"attention": [...], "mlp_up": [...]} lists of
+        # (start, end) torch.cuda.Event pairs recorded on the launch stream
+        self.probe: Optional[Dict[str, list]] = None
+        self._ws: Dict[Tuple, _Workspace] = {}
+        self._rope: Dict[Tuple, Tuple[torch.Tensor, ...]] = {}
+        # K % 64 requirement of the GEMM kernels for the small input projections
+        if in_channels % 64 or joint_attention_dim % 64:
+            raise NotImplementedError("in_channels and joint_attention_dim must be multiples of 64")
+
+    # ------------------------------------------------------------------ diffusers-like surface
+    @property
+    def dtype(self) -> torch.dtype:
+        return BF16
+
+    @property
+    def device(self) -> torch.device:
+        return self.img_in_w.device
+
+    @contextlib.contextmanager
+    def cache_context(self, name: str):
+        yield
+
+    def _param_slot(self, name: str) -> torch.Tensor:
+        """Map a diffusers state_dict name to the (view of the) packed tensor."""
+        D = self.config.inner_dim
+        top = {
+            "img_in.weight": self.img_in_w, "img_in.bias": self.img_in_b,
+            "txt_norm.weight": self.txt_norm_w,
+            "txt_in.weight": self.txt_in_w, "txt_in.bias": self.txt_in_b,
+            "time_text_embed.timestep_embedder.linear_1.weight": self.t_l1_w,
+            "time_text_embed.timestep_embedder.linear_1.bias": self.t_l1_b,
+            "time_text_embed.timestep_embedder.linear_2.weight": self.t_l2_w,
+            "time_text_embed.timestep_embedder.linear_2.bias": self.t_l2_b,
+            "norm_out.linear.weight": self.norm_out_w, "norm_out.linear.bias": self.norm_out_b,
+            "proj_out.weight": self.proj_out_w, "proj_out.bias": self.proj_out_b,
+        }
+        if name in top:
+            return top[name]
+        parts = name.split(".")
+        if parts[0] != "transformer_blocks":
+            raise KeyError(name)
+        blk = self.transformer_blocks[int(parts[1])]
+        rest = ".".join(parts[2:])
+        kind = "w" if rest.endswith("weight") else "b"
+        stem = rest.rsplit(".", 1)[0]
+        qkv = {"attn.to_q": ("img", 0), "attn.to_k": ("img", 1), "attn.to_v": ("img", 2),
+               "attn.add_q_proj": ("txt", 0), "attn.add_k_proj": ("txt", 1),
+               "attn.add_v_proj": ("txt", 2)}
+        if stem in qkv:
+            s, j = qkv[stem]
+            return getattr(blk, f"{kind}_qkv_{s}")[j * D:(j + 1) * D]
+        simple = {"img_mod.1": "mod_img", "txt_mod.1": "mod_txt", "attn.to_out.0": "out_img",
+                  "attn.to_add_out": "out_txt", "img_mlp.net.0.proj": "up_img",
+                  "img_mlp.net.2": "down_img", "txt_mlp.net.0.proj": "up_txt",
+                  "txt_mlp.net.2": "down_txt"}
+        if stem in simple:
+            return getattr(blk, f"{kind}_{simple[stem]}")
+        if stem.startswith("attn.norm_"):
+            return getattr(blk, stem[len("attn."):])
+        raise KeyError(name)
+
+    def diffusers_names(self) -> List[str]:
+        names = ["img_in.weight", "img_in.bias", "txt_norm.weight", "txt_in.weight", "txt_in.bias"]
+        names += [f"time_text_embed.timestep_embedder.linear_{i}.{k}" for i in (1, 2) for k in ("weight", "bias")]
+        for i in range(self.config.num_layers):
+            p = f"transformer_blocks.{i}."
+            for s in ("img", "txt"):
+                names += [p + f"{s}_mod.1.weight", p + f"{s}_mod.1.bias"]
+            for n in ("to_q", "to_k", "to_v", "add_q_proj", "add_k_proj", "add_v_proj",
+                      "to_out.0", "to_add_out"):
+                names += [p + f"attn.{n}.weight", p + f"attn.{n}.bias"]
+            names += [p + f"attn.{n}.weight" for n in ("norm_q", "norm_k", "norm_added_q", "norm_added_k")]
+            for s in ("img", "txt"):
+                names += [p + f"{s}_mlp.net.{j}.weight" for j in ("0.proj", "2")]
+                names += [p + f"{s}_mlp.net.{j}.bias" for j in ("0.proj", "2")]
+        names += ["norm_out.linear.weight", "norm_out.linear.bias", "proj_out.weight", "proj_out.bias"]
+        return names
+
+    @torch.no_grad()
+    def load_diffusers_state_dict(self, sd: Dict[str, torch.Tensor], strict: bool = True):
+        """Copy diffusers-named tensors into the packed buffers."""
+        seen = set()
+        for k, v in sd.items():
+            try:
+                slot = self._param_slot(k)
+            except (KeyError, IndexError):
+                if strict:
+                    raise KeyError(f"unexpected parameter {k}")
+                continue
+            if tuple(slot.shape) != tuple(v.shape):
+                raise ValueError(f"{k}: shape {tuple(v.shape)} != {tuple(slot.shape)}")
+            slot.copy_(v.to(slot.device, BF16))
+            seen.add(k)
+        if strict:
+            missing = set(self.diffusers_names()) - seen
+            if missing:
+                raise KeyError(f"missing parameters: {sorted(missing)[:5]} ...")
+        self._requantize_if_needed()
+
+    def diffusers_state_dict(self) -> Iterator[Tuple[str, torch.Tensor]]:
+        for n in self.diffusers_names():
+            yield n, self._param_slot(n)
+
+    @torch.no_grad()
+    def random_init_(self, seed: int = 0, std: float = 0.02):
+        """Seeded N(0, std) init of every Linear weight/bias, 1 + N(0, std) for
+        RMSNorm weights (SURVEY.md §8 d), generated directly in HBM."""
+        g = torch.Generator(device=self.device).manual_seed(seed)
+        for n in self.diffusers_names():
+            t = self._param_slot(n)
+            t.normal_(0.0, std, generator=g)
+            if n == "txt_norm.weight" or ".attn.norm_" in n:
+                t.add_(1.0)
+        self._requantize_if_needed()
+        return self
+
+    # ------------------------------------------------------------------ int8 (a16)
+    _I8_LINEARS = ("qkv_img", "qkv_txt", "out_img", "out_txt", "up_img", "up_txt", "down_img", "down_txt")
+
+    @torch.no_grad()
+    def quantize_int8(self):
+        """Int8Linear replacement pass (README.md:136-138 'replace nn.Linear with
+        Int8Linear in transformer'): per-output-channel int8 weights + fp32
+        scales for every block linear, computed by the HIP quantiser."""
+        for blk in self.transformer_blocks:
+            blk.q8 = {}
+            for n in self._I8_LINEARS:
+                w = getattr(blk, f"w_{n}")
+                q = torch.empty(w.shape, dtype=torch.int8, device=w.device)
+                s = torch.empty(w.shape[0], dtype=torch.float32, device=w.device)
+                ops.quantize_rows(w, q, s)
+                blk.q8[n] = (q, s)
+        self.int8 = True
+        self._ws.clear()
+        return self
+
+    def _requantize_if_needed(self):
+        if self.int8:
+            self.quantize_int8()
+
+    # ------------------------------------------------------------------ forward
+    def _workspace(self, B, S_img, S_txt) -> _Workspace:
+        key = (B, S_img, S_txt, self.int8)
+        ws = self._ws.get(key)
+        if ws is None:
+            if len(self._ws) > 4:
+                self._ws.clear()
+            ws = _Workspace(self.config, B, S_img, S_txt, self.device, self.int8)
+            self._ws[key] = ws
+        return ws
+
+    def _rope_tables(self, img_shapes, S_txt):
+        key = (tuple(tuple(x) for x in img_shapes), S_txt)
+        t = self._rope.get(key)
+        if t is None:
+            t = rope_tables(img_shapes, S_txt, self.device, self.config.axes_dims_rope)
+            self._rope[key] = t
+        return t
+
+    @torch.no_grad()
+    def forward(self, hidden_states: torch.Tensor, encoder_hidden_states: torch.Tensor = None,
+                encoder_hidden_states_mask: Optional[torch.Tensor] = None,
+                timestep: torch.Tensor = None, img_shapes=None, txt_seq_lens: Optional[Sequence[int]] = None,
+                guidance: Optional[torch.Tensor] = None, attention_kwargs=None,
+                controlnet_block_samples=None, return_dict: bool = True, out: Optional[torch.Tensor] = None):
+        cfg = self.config
+        D, H = cfg.inner_dim, cfg.num_attention_heads
+        B, S_img, Cin = hidden_states.shape
+        S_txt = encoder_hidden_states.shape[1]
+        if controlnet_block_samples is not None:
+            raise NotImplementedError("controlnet residuals are not on the reference's path")
+        if txt_seq_lens is None:
+            if encoder_hidden_states_mask is not None:
+                txt_seq_lens = [int(x) for x in encoder_hidden_states_mask.sum(dim=1).tolist()]
+            else:
+                txt_seq_lens = [S_txt] * B
+        txt_seq_lens = [int(x) for x in txt_seq_lens]
+        if len(txt_seq_lens) != B or max(txt_seq_lens) > S_txt or min(txt_seq_lens) < 0:
+            raise ValueError("txt_seq_lens must give one length <= S_txt per batch row")
+        if img_shapes is None:
+            raise ValueError("img_shapes is required")
+        shapes = img_shapes[0] if isinstance(img_shapes[0], (list, tuple)) and \
+            isinstance(img_shapes[0][0], (list, tuple)) else img_shapes
+        if sum(f * h * w for f, h, w in shapes) != S_img:
+            raise ValueError(f"img_shapes {shapes} do not cover {S_img} image tokens")
+        if B > 16:
+            raise ValueError("at most 16 batch rows per forward")
+
+        x_in = hidden_states.to(BF16).contiguous().view(B * S_img, Cin)
+        enc = encoder_hidden_states.to(BF16).contiguous().view(B * S_txt, cfg.joint_attention_dim)
+        ws = self._workspace(B, S_img, S_txt)
+        t = timestep.reshape(-1)
+        if t.numel() not in (1, B):
+            raise ValueError("timestep must have 1 or B entries")
+        if t.dtype == BF16 and t.numel() == B and t.is_cuda and t.is_contiguous():
+            t_bf = t
+        else:
+            t_bf = ws.t_bf
+            t_bf.copy_(t.to(BF16).expand(B))
+        icos, isin, tcos, tsin = self._rope_tables(shapes, S_txt)
+        if out is None:
+            out = torch.empty(B, S_img, cfg.patch_size ** 2 * cfg.out_channels, dtype=BF16,
+                              device=self.device)
+        self._forward_impl(ws, x_in, enc, t_bf, B, S_img, S_txt, txt_seq_lens, icos, isin, tcos, tsin,
+                           out.view(B * S_img, -1))
+        if not return_dict:
+            return (out,)
+        return Transformer2DModelOutput(sample=out)
+
+    def _forward_impl(self, ws: _Workspace, x_in, enc, t_bf, B, S_img, S_txt, txt_lens, icos, isin, tcos,
+                      tsin, out2d):
+        cfg = self.config
+        D = cfg.inner_dim
+        eps = 1e-6
+        has_txt = S_txt > 0
+        R_t = B * S_txt
+        # ---- prologue: img_in, txt_norm + txt_in, timestep embedding
+        ops.linear(x_in, self.img_in_w, self.img_in_b, out=ws.x_img)
+        if has_txt:
+            ops.rmsnorm(enc, self.txt_norm_w, out=ws.txt_norm[:R_t], eps=eps)
+            ops.linear(ws.txt_norm[:R_t], self.txt_in_w, self.txt_in_b, out=ws.x_txt[:R_t])
+        ops.timestep_embed(t_bf, 256, out=ws.tproj)
+        ops.gemv(ws.tproj, self.t_l1_w, self.t_l1_b, out=ws.t_h)
+        ops.silu(ws.t_h, out=ws.t_hs)
+        ops.gemv(ws.t_hs, self.t_l2_w, self.t_l2_b, out=ws.temb)
+        ops.silu(ws.temb, out=ws.stemb)
+        kv_len = [S_img + l for l in txt_lens]
+        for blk in self.transformer_blocks:
+            self._block(blk, ws, B, S_img, S_txt, kv_len, icos, isin, tcos, tsin, eps)
+        # ---- head: AdaLayerNormContinuous (scale first) + proj_out
+        ops.gemv(ws.stemb, self.norm_out_w, self.norm_out_b, out=ws.emb_out)
+        ops.layernorm_modulate(ws.x_img, ws.emb_out[:, D:], ws.emb_out[:, :D], S_img, out=ws.h_img,
+                               eps=eps)
+        ops.linear(ws.h_img, self.proj_out_w, self.proj_out_b, out=out2d)
+
+    def _block(self, blk: _Block, ws: _Workspace, B, S_img, S_txt, kv_len, icos, isin, tcos, tsin, eps):
+        D = self.config.inner_dim
+        R_t = B * S_txt
+        has_txt = S_txt > 0
+        i8 = self.int8
+        ops.gemv(ws.stemb, blk.w_mod_img, blk.b_mod_img, out=ws.mod_img)
+        if has_txt:
+            ops.gemv(ws.stemb, blk.w_mod_txt, blk.b_mod_txt, out=ws.mod_txt)
+        mi, mt = ws.mod_img, ws.mod_txt  # chunks: shift1 scale1 gate1 shift2 scale2 gate2
+        streams = [("img", ws.x_img, ws.h_img, ws.att_img, ws.mlp_img, mi, S_img, 0)]
+        if has_txt:
+            streams.append(("txt", ws.x_txt[:R_t], ws.h_txt[:R_t], ws.att_txt[:R_t],
+                            ws.mlp_txt[:R_t], mt, S_txt, S_img))
+        # ---- LN1 + modulate, fused QKV projection into the joint buffer
+        for s, x, h, att, mlp, m, rpb, seq_off in streams:
+            if i8:
+                qD, sc = self._q8(ws, s, x.shape[0], D)
+                ops.layernorm_modulate_i8(x, m[:, 0:D], m[:, D:2 * D], rpb, qD, sc, eps)
+                ops.linear_qkv_i8(qD, sc, *blk.q8[f"qkv_{s}"], getattr(blk, f"b_qkv_{s}"), ws.qkv, rpb,
+                                  seq_off)
+            else:
+                ops.layernorm_modulate(x, m[:, 0:D], m[:, D:2 * D], rpb, out=h, eps=eps)
+                ops.linear_qkv(h, getattr(blk, f"w_qkv_{s}"), getattr(blk, f"b_qkv_{s}"), ws.qkv, rpb,
+                               seq_off)
+        # ---- QK RMSNorm + RoPE, joint attention
+        ops.qk_norm_rope(ws.qkv, 0, S_img, blk.norm_q, blk.norm_k, icos, isin, eps)
+        if has_txt:
+            ops.qk_norm_rope(ws.qkv, S_img, S_txt, blk.norm_added_q, blk.norm_added_k, tcos, tsin, eps)
+        with self._probe("attention"):
+            ops.attention(ws.qkv, kv_len, ws.att_img, ws.att_txt[:R_t] if has_txt else None, S_img, S_txt)
+        # ---- out-proj + gated residual, LN2 + modulate, MLP + gated residual
+        for s, x, h, att, mlp, m, rpb, seq_off in streams:
+            if i8:
+                rows, F = x.shape[0], mlp.shape[1]
+                qD, sc = self._q8(ws, s, rows, D)
+                ops.quantize_rows(att, qD, sc)
+                ops.linear_gated_residual_i8(qD, sc, *blk.q8[f"out_{s}"], getattr(blk, f"b_out_{s}"),
+                                             m[:, 2 * D:3 * D], rpb, x)
+                ops.layernorm_modulate_i8(x, m[:, 3 * D:4 * D], m[:, 4 * D:5 * D], rpb, qD, sc, eps)
+                with self._probe("mlp_up" if s == "img" else None):
+                    ops.linear_i8(qD, sc, *blk.q8[f"up_{s}"], getattr(blk, f"b_up_{s}"), mlp,
+                                  act=ops.ACT_GELU)
+                qF, sc = self._q8(ws, s, rows, F)
+                ops.quantize_rows(mlp, qF, sc)
+                ops.linear_gated_residual_i8(qF, sc, *blk.q8[f"down_{s}"], getattr(blk, f"b_down_{s}"),
+                                             m[:, 5 * D:6 * D], rpb, x)
+            else:
+                ops.linear_gated_residual(att, getattr(blk, f"w_out_{s}"), getattr(blk, f"b_out_{s}"),
+                                          m[:, 2 * D:3 * D], rpb, x)
+                ops.layernorm_modulate(x, m[:, 3 * D:4 * D], m[:, 4 * D:5 * D], rpb, out=h, eps=eps)
+                with self._probe("mlp_up" if s == "img" else None):
+                    ops.linear(h, getattr(blk, f"w_up_{s}"), getattr(blk, f"b_up_{s}"), out=mlp,
+                               act=ops.ACT_GELU)
+                ops.linear_gated_residual(mlp, getattr(blk, f"w_down_{s}"), getattr(blk, f"b_down_{s}"),
+                                          m[:, 5 * D:6 * D], rpb, x)
+
+    @contextlib.contextmanager
+    def _probe(self, name: Optional[str]):
+        """Record a (start, end) event pair around one kernel launch when probing."""
+        if self.probe is None or name is None or name not in self.probe:
+            yield
+            return
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        yield
+        b.record()
+        self.probe[name].append((a, b))
+
+    @staticmethod
+    def _q8(ws: _Workspace, s: str, rows: int, K: int):
+        """[rows, K] int8 view of the stream's quantisation buffer + its scales."""
+        q = ws.q_img if s == "img" else ws.q_txt
+        sc = ws.s_img if s == "img" else ws.s_txt
+        return q.view(-1)[: rows * K].view(rows, K), sc[:rows]
+
+    # ------------------------------------------------------------------ bookkeeping
+    def flops_per_forward(self, S_img: int, S_txt: int, B: int = 1) -> float:
+        """Algorithmic FLOPs (SURVEY.md §8 d formula; padded rows not counted)."""
+        c = self.config
+        D, L = c.inner_dim, c.num_layers
+        S = S_img + S_txt
+        f = (L * (24 * S * D * D + 4 * S * S * D + 24 * D * D) + 2 * S_img * c.in_channels * D
+             + 2 * S_txt * c.joint_attention_dim * D + 2 * (256 * D + D * D) + 4 * D * D
+             + 2 * S_img * D * c.patch_size ** 2 * c.out_channels)
+        return float(f) * B

@@ -1,0 +1,116 @@
+"""Weight loading: local diffusers-format safetensors + Lightning-LoRA fuse.
+
+The reference loads by hub name (server.py:64-69 ``from_pretrained(
+"Qwen/Qwen-Image-Edit-2509")``, server.py:76-79 ``load_lora_weights(
+"lightx2v/Qwen-Image-Lightning", weight_name="Qwen-Image-Edit-Lightning-4steps-
+V1.0.safetensors")``).  There is no network here, so this module reads LOCAL
+paths only with the safe loader (``safetensors``; never
+pickle), and fuses LoRA deltas into the packed bf16 weights at load time
+(W += scale * B @ A), so the Lightning adapters cost nothing per step (§2D K14).
+"""
+from __future__ import annotations
+
+import glob
+import os
+import re
+from typing import Dict, Iterable, Optional, Tuple
+
+import torch
+
+BF16 = torch.bfloat16
+
+
+def find_transformer_files(path: str):
+    """Locate transformer safetensors shards under a diffusers repo snapshot."""
+    if os.path.isfile(path) and path.endswith(".safetensors"):
+        return [path]
+    for sub in ("transformer", "."):
+        files = sorted(glob.glob(os.path.join(path, sub, "*.safetensors")))
+        if files:
+            return files
+    return []
+
+
+def iter_safetensors(files: Iterable[str]):
+    from safetensors import safe_open
+    for f in files:
+        with safe_open(f, framework="pt", device="cpu") as fh:
+            for k in fh.keys():
+                yield k, fh.get_tensor(k)
+
+
+def load_transformer_weights(model, path: str, strict: bool = True) -> int:
+    files = find_transformer_files(path)
+    if not files:
+        raise FileNotFoundError(f"no transformer *.safetensors under {path}")
+    n = 0
+    names = set(model.diffusers_names())
+    seen = set()
+    with torch.no_grad():
+        for k, v in iter_safetensors(files):
+            if k not in names:
+                if strict:
+                    raise KeyError(f"unexpected parameter {k}")
+                continue
+            model._param_slot(k).copy_(v.to(model.device, BF16))
+            seen.add(k)
+            n += 1
+    if strict and seen != names:
+        raise KeyError(f"missing {len(names - seen)} parameters, e.g. {sorted(names - seen)[:3]}")
+    model._requantize_if_needed()
+    return n
+
+
+_LORA_PATTERNS = [
+    # peft / diffusers style
+    (re.compile(r"^(?:transformer\.)?(.+)\.lora_A(?:\.default)?\.weight$"), "A"),
+    (re.compile(r"^(?:transformer\.)?(.+)\.lora_B(?:\.default)?\.weight$"), "B"),
+    # kohya-ish style
+    (re.compile(r"^(?:transformer\.|diffusion_model\.)?(.+)\.lora_down\.weight$"), "A"),
+    (re.compile(r"^(?:transformer\.|diffusion_model\.)?(.+)\.lora_up\.weight$"), "B"),
+    (re.compile(r"^(?:transformer\.|diffusion_model\.)?(.+)\.alpha$"), "alpha"),
+]
+
+
+def parse_lora(sd: Dict[str, torch.Tensor]) -> Dict[str, Dict[str, torch.Tensor]]:
+    """Group a LoRA state dict into {module_stem: {"A": [r,in], "B": [out,r], "alpha": ()}}."""
+    groups: Dict[str, Dict[str, torch.Tensor]] = {}
+    for k, v in sd.items():
+        for pat, kind in _LORA_PATTERNS:
+            m = pat.match(k)
+            if m:
+                groups.setdefault(m.group(1), {})[kind] = v
+                break
+    return groups
+
+
+@torch.no_grad()
+def fuse_lora(model, lora_sd: Dict[str, torch.Tensor], scale: float = 1.0, strict: bool = False) -> int:
+    """W[stem] += scale * (alpha / r) * B @ A for every adapter in the dict."""
+    fused = 0
+    for stem, g in parse_lora(lora_sd).items():
+        if "A" not in g or "B" not in g:
+            continue
+        try:
+            w = model._param_slot(stem + ".weight")
+        except (KeyError, IndexError, AttributeError):
+            if strict:
+                raise
+            continue
+        A = g["A"].to(model.device, torch.float32)
+        B = g["B"].to(model.device, torch.float32)
+        r = A.shape[0]
+        s = scale * (float(g["alpha"]) / r if "alpha" in g else 1.0)
+        w.copy_((w.float() + s * (B @ A)).to(BF16))
+        fused += 1
+    model._requantize_if_needed()
+    return fused
+
+
+def load_lora_file(path: str, weight_name: Optional[str] = None) -> Dict[str, torch.Tensor]:
+    f = os.path.join(path, weight_name) if weight_name and os.path.isdir(path) else path
+    if not os.path.isfile(f):
+        raise FileNotFoundError(
+            f"LoRA file {f} not found (hub names such as 'lightx2v/Qwen-Image-Lightning' need a "
+            "local snapshot: there is no network access)")
+    return dict(iter_safetensors([f]))

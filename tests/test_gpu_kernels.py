@@ -1,0 +1,298 @@
+"""Per-kernel parity: every libqie entry point vs the CPU oracle (or, for the
+floating-point contractions, the oracle's fp32 math with the reference's bf16
+rounding points).  Runs through the C ABI on the GPU.
+
+Tolerances (bf16 storage, fp32 accumulation; the HIP kernels sum in a
+different order than the CPU, so results may differ by the last bf16 bit):
+  * GEMM / GEMV / norms:   rel-L2 <= 4e-3 and max |diff| <= 2 bf16 ulps of the
+                           tensor's max magnitude (2 * 2^-8 * max|ref|)
+  * attention:             rel-L2 <= 1e-2 vs fp32 softmax (P is rounded to bf16
+                           before P.V, as in the reference's flash SDPA)
+  * Euler step, pack/unpack, int8 quantisation: bit-exact
+  * int8 GEMM:             within 1 bf16 ulp of the exact-integer oracle
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import dit_ref as R
+from oracle import int8_ref as Q8
+
+pytestmark = pytest.mark.gpu
+BF16 = torch.bfloat16
+
+
+def _ops():
+    from qwen_image_edit_streamdiffusion_amd import ops
+    return ops
+
+
+def rnd(shape, dev, scale=1.0, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.randn(shape, generator=g) * scale).to(BF16).to(dev)
+
+
+def close(actual, ref, rel_l2=4e-3, ulps=2):
+    a, r = actual.float().cpu(), ref.float().cpu()
+    assert a.shape == r.shape, (a.shape, r.shape)
+    assert torch.isfinite(a).all(), "non-finite output"
+    err = (a - r).norm() / max(r.norm().item(), 1e-30)
+    mx = (a - r).abs().max().item()
+    bound = ulps * 2.0 ** -8 * r.abs().max().item() + 1e-6
+    assert err <= rel_l2 and mx <= bound, f"rel_l2={err:.3e} max_abs={mx:.3e} bound={bound:.3e}"
+
+
+RB = R._R(True)
+
+
+@pytest.mark.parametrize("M,N,K", [(300, 384, 192), (2000, 2304, 128), (4300, 3072, 256),
+                                   (4096, 4096, 64), (17, 512, 3072)])
+@pytest.mark.parametrize("act", [0, 1])
+def test_linear(dev, M, N, K, act):
+    ops = _ops()
+    x, w, b = rnd((M, K), dev, 1.0, 1), rnd((N, K), dev, 0.05, 2), rnd((N,), dev, 0.1, 3)
+    y = ops.linear(x, w, b, act=act)
+    ref = R.linear(x.cpu(), w.cpu(), b.cpu(), RB)
+    if act:
+        ref = R.gelu_tanh(ref, RB)
+    close(y, ref)
+
+
+def test_linear_strided_input(dev):
+    ops = _ops()
+    big = rnd((512, 384), dev, 1.0, 4)
+    x = big[:, 128:]  # row stride 384, K = 256
+    w, b = rnd((256, 256), dev, 0.05, 5), rnd((256,), dev, 0.1, 6)
+    close(ops.linear(x, w, b), R.linear(x.cpu(), w.cpu(), b.cpu(), RB))
+
+
+@pytest.mark.parametrize("M,N,K", [(1, 18432, 3072), (2, 6144, 3072), (4, 3072, 256), (9, 512, 1024)])
+def test_gemv(dev, M, N, K):
+    ops = _ops()
+    x, w, b = rnd((M, K), dev, 1.0, 7), rnd((N, K), dev, 0.02, 8), rnd((N,), dev, 0.02, 9)
+    close(ops.gemv(x, w, b), R.linear(x.cpu(), w.cpu(), b.cpu(), RB))
+
+
+@pytest.mark.parametrize("B,rpb,N,K", [(2, 300, 512, 256), (2, 4096, 3072, 512), (3, 40, 256, 1024)])
+def test_gated_residual(dev, B, rpb, N, K):
+    ops = _ops()
+    M = B * rpb
+    x, w, b = rnd((M, K), dev, 1.0, 10), rnd((N, K), dev, 0.05, 11), rnd((N,), dev, 0.1, 12)
+    mods = rnd((B, 6 * N), dev, 0.5, 13)
+    gate = mods[:, 2 * N:3 * N]
+    resid = rnd((M, N), dev, 1.0, 14)
+    ref = R.gated_residual(resid.cpu().float().view(B, rpb, N), gate.cpu(),
+                           R.linear(x.cpu(), w.cpu(), b.cpu(), RB).view(B, rpb, N), RB).view(M, N)
+    ops.linear_gated_residual(x, w, b, gate, rpb, resid)
+    close(resid, ref)
+
+
+def test_qkv_scatter(dev):
+    ops = _ops()
+    B, H, Dh, rpb, s_pad, off, K = 2, 2, 128, 200, 512, 300, 256
+    x, w, b = rnd((B * rpb, K), dev, 1.0, 15), rnd((3 * H * Dh, K), dev, 0.05, 16), rnd((3 * H * Dh,), dev, 0.1, 17)
+    qkv = torch.zeros(3, B, H, s_pad, Dh, dtype=BF16, device=dev)
+    ops.linear_qkv(x, w, b, qkv, rpb, off)
+    ref = R.linear(x.cpu(), w.cpu(), b.cpu(), RB).view(B, rpb, 3, H, Dh).permute(2, 0, 3, 1, 4)
+    close(qkv[:, :, :, off:off + rpb].cpu(), ref)
+    assert (qkv[:, :, :, :off] == 0).all() and (qkv[:, :, :, off + rpb:] == 0).all()
+
+
+@pytest.mark.parametrize("B,rpb,D", [(2, 100, 3072), (1, 33, 256), (3, 7, 1024)])
+def test_layernorm_modulate(dev, B, rpb, D):
+    ops = _ops()
+    x = rnd((B * rpb, D), dev, 2.0, 18)
+    mods = rnd((B, 6 * D), dev, 0.5, 19)
+    y = ops.layernorm_modulate(x, mods[:, :D], mods[:, D:2 * D], rpb)
+    xc = x.cpu().float().view(B, rpb, D)
+    ref = R.modulate(R.layer_norm(xc, 1e-6, RB), mods.cpu()[:, :D], mods.cpu()[:, D:2 * D], RB)
+    close(y, ref.view(B * rpb, D))
+
+
+def test_layernorm_modulate_i8_matches_quantized_bf16(dev):
+    ops = _ops()
+    B, rpb, D = 2, 64, 3072
+    x = rnd((B * rpb, D), dev, 2.0, 20)
+    mods = rnd((B, 6 * D), dev, 0.5, 21)
+    y = ops.layernorm_modulate(x, mods[:, :D], mods[:, D:2 * D], rpb)
+    q = torch.empty(B * rpb, D, dtype=torch.int8, device=dev)
+    s = torch.empty(B * rpb, dtype=torch.float32, device=dev)
+    ops.layernorm_modulate_i8(x, mods[:, :D], mods[:, D:2 * D], rpb, q, s)
+    qr, sr = Q8.quantize_rows(y.float().cpu().numpy())
+    assert np.array_equal(q.cpu().numpy(), qr)
+    assert np.array_equal(s.cpu().numpy(), sr)
+
+
+@pytest.mark.parametrize("R_,D", [(64, 3584), (5, 128), (300, 1024)])
+def test_rmsnorm(dev, R_, D):
+    ops = _ops()
+    x, w = rnd((R_, D), dev, 3.0, 22), (1 + rnd((D,), dev, 0.02, 23).float()).to(BF16)
+    close(ops.rmsnorm(x, w), R.rms_norm(x.cpu(), w.cpu(), 1e-6, RB))
+
+
+def test_qk_norm_rope(dev):
+    ops = _ops()
+    from qwen_image_edit_streamdiffusion_amd.rope import rope_tables
+    B, H, s_pad = 2, 3, 512
+    shapes, txt = [(1, 8, 8), (1, 8, 16)], 37
+    S_img = 64 + 128
+    qkv = rnd((3, B, H, s_pad, 128), dev, 2.0, 24)
+    orig = qkv.clone()
+    ws = [(1 + rnd((128,), dev, 0.1, 25 + i).float()).to(BF16) for i in range(4)]
+    ic, is_, tc, ts = rope_tables(shapes, txt, dev)
+    ops.qk_norm_rope(qkv, 0, S_img, ws[0], ws[1], ic, is_)
+    ops.qk_norm_rope(qkv, S_img, txt, ws[2], ws[3], tc, ts)
+    ip, tp = R.rope_phases(shapes, txt)
+    for which in (0, 1):
+        for seg, (a, n, wq, ph) in enumerate([(0, S_img, ws[which], ip), (S_img, txt, ws[2 + which], tp)]):
+            x = orig[which, :, :, a:a + n].cpu().permute(0, 2, 1, 3)  # [B, S, H, Dh]
+            ref = R.apply_rope(R.rms_norm(x, wq.cpu(), 1e-6, RB), ph, RB).permute(0, 2, 1, 3)
+            close(qkv[which, :, :, a:a + n], ref)
+    assert torch.equal(qkv[2], orig[2])  # V untouched
+    assert torch.equal(qkv[:, :, :, S_img + txt:], orig[:, :, :, S_img + txt:])
+
+
+def _attn_ref(qkv, kv_len, s_img, txt_rows):
+    _, B, H, s_pad, Dh = qkv.shape
+    S = s_img + txt_rows
+    q, k, v = (qkv[i].float().cpu() for i in range(3))
+    outs = []
+    for b in range(B):
+        L = kv_len[b]
+        s = q[b, :, :S] @ k[b, :, :L].transpose(-1, -2) / math.sqrt(Dh)
+        o = torch.softmax(s, -1) @ v[b, :, :L]  # [H, S, Dh]
+        outs.append(o.permute(1, 0, 2).reshape(S, H * Dh))
+    o = torch.stack(outs)
+    return o[:, :s_img].reshape(B * s_img, -1), o[:, s_img:].reshape(B * txt_rows, -1)
+
+
+@pytest.mark.parametrize("B,H,s_img,txt_rows,kv_len,scale", [
+    (1, 2, 512, 40, [552], 1.0),
+    (2, 2, 512, 40, [552, 530], 1.0),
+    (2, 3, 1024, 216, [1240, 1235], 3.0),
+    (1, 1, 256, 0, [256], 1.0),
+])
+def test_attention(dev, B, H, s_img, txt_rows, kv_len, scale):
+    ops = _ops()
+    s_pad = ((s_img + txt_rows + 255) // 256) * 256
+    qkv = rnd((3, B, H, s_pad, 128), dev, scale, 30)
+    qkv[:, :, :, s_img + txt_rows:] = 0
+    oi = torch.empty(B * s_img, H * 128, dtype=BF16, device=dev)
+    ot = torch.empty(max(B * txt_rows, 1), H * 128, dtype=BF16, device=dev)
+    ops.attention(qkv, kv_len, oi, ot[: B * txt_rows] if txt_rows else None, s_img, txt_rows)
+    ri, rt = _attn_ref(qkv, kv_len, s_img, txt_rows)
+    close(oi, ri, rel_l2=1e-2, ulps=8)
+    if txt_rows:
+        close(ot[: B * txt_rows], rt, rel_l2=1e-2, ulps=8)
+
+
+def test_attention_spike_rescale(dev):
+    """Force the online-softmax rescale: one key far above the rest in a late tile."""
+    ops = _ops()
+    B, H, s_img = 1, 1, 512
+    qkv = rnd((3, B, H, s_img, 128), dev, 1.0, 31)
+    qkv[1, 0, 0, 450] = qkv[0, 0, 0, 3] * 6  # key 450 aligned with query 3
+    oi = torch.empty(s_img, 128, dtype=BF16, device=dev)
+    ops.attention(qkv, [s_img], oi, None, s_img, 0)
+    ri, _ = _attn_ref(qkv, [s_img], s_img, 0)
+    close(oi, ri, rel_l2=1e-2, ulps=8)
+
+
+def test_timestep_embed(dev):
+    ops = _ops()
+    t = torch.tensor([1.0, 0.02001953125, 0.7695, 0.0], dtype=BF16)
+    y = ops.timestep_embed(t.to(dev), 256)
+    close(y, R.timestep_sinusoid(t, 256).to(BF16), rel_l2=4e-3, ulps=2)
+
+
+def test_silu(dev):
+    ops = _ops()
+    x = rnd((3, 3072), dev, 3.0, 32)
+    close(ops.silu(x), R.silu(x.cpu(), RB))
+
+
+def test_cfg_combine(dev):
+    ops = _ops()
+    B, S, S_img = 2, 256, 512
+    out = rnd((2 * B, S_img, 64), dev, 1.0, 33)
+    y = ops.cfg_combine(out[:B, :S], out[B:, :S], 4.0)
+    ref = R.cfg_combine(out[:B, :S].cpu(), out[B:, :S].cpu(), 4.0)
+    close(y, ref, rel_l2=2e-3, ulps=1)
+
+
+def test_euler_step_bit_exact(dev):
+    ops = _ops()
+    B, S, S_img = 3, 256, 512
+    inp = rnd((B, S_img, 64), dev, 1.0, 34)
+    v = rnd((B, S, 64), dev, 1.0, 35)
+    dts = [-0.98, -0.3, 0.0]
+    x0 = inp[:, :S].clone()
+    ops.euler_step(inp[:, :S], v, dts, inp[:, :S])
+    for b in range(B):
+        ref = R.euler_step(x0[b].cpu(), v[b].cpu(), 0.0, dts[b])
+        assert torch.equal(inp[b, :S].cpu(), ref), b
+
+
+def test_pack_unpack_exact(dev):
+    ops = _ops()
+    x = rnd((2, 16, 1, 32, 48), dev, 1.0, 36)
+    p = ops.pack_latents(x)
+    assert torch.equal(p.cpu(), R.pack_latents(x.cpu()))
+    u = ops.unpack_latents(p, 32, 48)
+    assert torch.equal(u.cpu(), x.cpu())
+
+
+def test_quantize_rows_exact(dev):
+    ops = _ops()
+    x = rnd((37, 12288), dev, 1.5, 37)
+    x[5] = 0
+    q = torch.empty(37, 12288, dtype=torch.int8, device=dev)
+    s = torch.empty(37, dtype=torch.float32, device=dev)
+    ops.quantize_rows(x, q, s)
+    qr, sr = Q8.quantize_rows(x.float().cpu().numpy())
+    assert np.array_equal(q.cpu().numpy(), qr)
+    assert np.array_equal(s.cpu().numpy(), sr)
+
+
+@pytest.mark.parametrize("M,N,K,act", [(300, 384, 256, 0), (4300, 3072, 384, 1), (2048, 2048, 3072, 0)])
+def test_linear_i8(dev, M, N, K, act):
+    ops = _ops()
+    g = torch.Generator().manual_seed(40)
+    xq = torch.randint(-127, 128, (M, K), generator=g, dtype=torch.int8)
+    wq = torch.randint(-127, 128, (N, K), generator=g, dtype=torch.int8)
+    sx = torch.rand(M, generator=g) * 0.01 + 1e-3
+    sw = torch.rand(N, generator=g) * 0.001 + 1e-4
+    b = (torch.randn(N, generator=g) * 0.1).to(BF16)
+    y = torch.empty(M, N, dtype=BF16, device=dev)
+    ops.linear_i8(xq.to(dev), sx.to(dev), wq.to(dev), sw.to(dev), b.to(dev), y, act=act)
+    acc = Q8.int8_gemm_acc(xq.numpy(), wq.numpy())
+    ref = torch.from_numpy(Q8.dequant(acc, sx.numpy(), sw.numpy(), b.float().numpy())).to(BF16).float()
+    if act:
+        ref = R.gelu_tanh(ref, RB)
+    close(y, ref, rel_l2=4e-3, ulps=2)
+
+
+def test_linear_i8_gated_and_qkv(dev):
+    ops = _ops()
+    g = torch.Generator().manual_seed(41)
+    B, rpb, K, H = 2, 260, 256, 2
+    N = H * 128
+    xq = torch.randint(-127, 128, (B * rpb, K), generator=g, dtype=torch.int8).to(dev)
+    sx = (torch.rand(B * rpb, generator=g) * 0.01 + 1e-3).to(dev)
+    wq = torch.randint(-127, 128, (3 * N, K), generator=g, dtype=torch.int8).to(dev)
+    sw = (torch.rand(3 * N, generator=g) * 1e-3 + 1e-4).to(dev)
+    b = (torch.randn(3 * N, generator=g) * 0.1).to(BF16).to(dev)
+    ref = torch.from_numpy(Q8.dequant(Q8.int8_gemm_acc(xq.cpu().numpy(), wq.cpu().numpy()),
+                                      sx.cpu().numpy(), sw.cpu().numpy(), b.float().cpu().numpy()))
+    ref = ref.to(BF16).float()
+    qkv = torch.zeros(3, B, H, 512, 128, dtype=BF16, device=dev)
+    ops.linear_qkv_i8(xq, sx, wq, sw, b, qkv, rpb, 0)
+    close(qkv[:, :, :, :rpb], ref.view(B, rpb, 3, H, 128).permute(2, 0, 3, 1, 4))
+    gate = rnd((B, N), dev, 0.5, 42)
+    resid = rnd((B * rpb, N), dev, 1.0, 43)
+    r0 = resid.cpu().float()
+    ops.linear_gated_residual_i8(xq, sx, wq[:N], sw[:N], b[:N], gate, rpb, resid)
+    exp = R.gated_residual(r0.view(B, rpb, N), gate.cpu(), ref[:, :N].reshape(B, rpb, N), RB)
+    close(resid, exp.view(B * rpb, N))
