@@ -412,9 +412,10 @@ def cfg_combine(cond: torch.Tensor, uncond: torch.Tensor, scale: float) -> torch
 # latent packing [U] (_pack_latents / _unpack_latents)
 # ----------------------------------------------------------------------------
 def pack_latents(x: torch.Tensor) -> torch.Tensor:
-    """[B, C, 1, H, W] (or [B, C, H, W]) -> [B, (H/2)(W/2), C*4]."""
+    """[B, 1, C, H, W] / [B, C, 1, H, W] / [B, C, H, W] -> [B, (H/2)(W/2), C*4]
+    (diffusers views the 5-D tensor as [B, C, H/2, 2, W/2, 2] by memory order)."""
     if x.dim() == 5:
-        x = x[:, :, 0]
+        x = x.reshape(x.shape[0], x.shape[1] * x.shape[2], x.shape[3], x.shape[4])
     B, C, H, W = x.shape
     x = x.view(B, C, H // 2, 2, W // 2, 2).permute(0, 2, 4, 1, 3, 5)
     return x.reshape(B, (H // 2) * (W // 2), C * 4)

@@ -241,10 +241,11 @@ def copy_batched(src: torch.Tensor, dst: torch.Tensor):
 
 
 def pack_latents(x: torch.Tensor) -> torch.Tensor:
-    """[B, C, H, W] (or [B, C, 1, H, W]) -> [B, (H/2)(W/2), 4C] (diffusers _pack_latents)."""
+    """[B, C, H, W] (or 5-D [B, 1, C, H, W] / [B, C, 1, H, W]) -> [B, (H/2)(W/2), 4C]
+    (diffusers _pack_latents views the 5-D noise by memory order)."""
     _dev(x)
     if x.dim() == 5:
-        x = x[:, :, 0]
+        x = x.reshape(x.shape[0], x.shape[1] * x.shape[2], x.shape[3], x.shape[4])
     x = x.contiguous()
     B, C, H, W = x.shape
     y = torch.empty(B, (H // 2) * (W // 2), 4 * C, dtype=BF16, device=x.device)

@@ -165,7 +165,7 @@ def _attn_ref(qkv, kv_len, s_img, txt_rows):
         o = torch.softmax(s, -1) @ v[b, :, :L]  # [H, S, Dh]
         outs.append(o.permute(1, 0, 2).reshape(S, H * Dh))
     o = torch.stack(outs)
-    return o[:, :s_img].reshape(B * s_img, -1), o[:, s_img:].reshape(B * txt_rows, -1)
+    return o[:, :s_img].reshape(B * s_img, H * Dh), o[:, s_img:].reshape(B * txt_rows, H * Dh)
 
 
 @pytest.mark.parametrize("B,H,s_img,txt_rows,kv_len,scale", [
