@@ -30,6 +30,7 @@ constexpr int kDh = 128;
 constexpr int kQB = 256;   // query rows per workgroup
 constexpr int kKB = 64;    // keys per tile
 constexpr int kTileBytes = kKB * kDh * 2;  // 16 KiB
+constexpr float kRescaleThr = 8.0f;        // lazy-rescale threshold, log2 units
 
 struct AttnArgs {
   const bf16_t* qkv;
@@ -101,6 +102,11 @@ __global__ void __launch_bounds__(512) attn_fwd_kernel(AttnArgs a) {
   gload(0);
   lwrite(0);
   __syncthreads();
+  // Drain every outstanding load (Q fragments included) with a waitcnt the
+  // compiler's scoreboard sees: otherwise it keeps Q "pending" into the loop and
+  // waits on the in-order vmcnt there -- i.e. on the NEXT tile's prefetch,
+  // exposing the full global-load latency every tile.
+  __builtin_amdgcn_s_waitcnt(0);
 
   f32x16_t o[4];
 #pragma unroll
@@ -152,23 +158,30 @@ __global__ void __launch_bounds__(512) attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[1][r]);
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float m_new = fmaxf(m_run, mx);
-    const float alpha = exp2f((m_run - m_new) * c);
-    const float mc = m_new * c;
-    m_run = m_new;
+    // lazy rescale (cdna_hip_programming.md T13): keep the running max unless a
+    // row of this wave grows by more than kRescaleThr (log2 units); P is then
+    // bounded by 2^kRescaleThr.  The decision covers this tile before any of its
+    // P is formed, and the previous tile's P.V is complete.
+    if (__any((mx - m_run) * c > kRescaleThr)) {
+      const float m_new = fmaxf(m_run, mx);
+      const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * c);
+      m_run = m_new;
+      l_run *= alpha;
+#pragma unroll
+      for (int db = 0; db < 4; ++db) o[db] *= alpha;
+    }
+    const float mc = m_run * c;
     float psum = 0.f;
     bf16x8_t pf[4];
 #pragma unroll
     for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const float p = exp2f(__builtin_fmaf(s[cb][r], c, -mc));
+        const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[cb][r], c, -mc));
         psum += p;
         pf[cb * 2 + (r >> 3)][r & 7] = (__bf16)p;
       }
-    l_run = l_run * alpha + psum;
-#pragma unroll
-    for (int db = 0; db < 4; ++db) o[db] *= alpha;
+    l_run += psum;
 
     // ---- O^T += V^T P^T
 #pragma unroll

@@ -195,6 +195,8 @@ __global__ void __launch_bounds__(WM* WN * 64)
     }
     const char QIE_LDS* at = smem + cur * STAGE;
     const char QIE_LDS* wt = at + A_BYTES;
+    // (an explicit two-register-set read pipeline measured 10-15 % slower at 252
+    //  VGPRs; hipcc's own lgkmcnt ladder with 2 waves/SIMD does better here)
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       const int cofs = ((kk * 4 + (lane >> 4)) ^ sw) << 4;

@@ -65,6 +65,9 @@ class FlowMatchEulerDiscreteScheduler:
         else:
             s = (c.shift * s / (1 + (c.shift - 1) * s)).astype(np.float32)
         if c.shift_terminal:
+            if len(s) < 2:
+                raise ValueError("a single-step schedule with shift_terminal stretches 0/0 "
+                                 "(NaN sigma); use >= 2 steps or shift_terminal=None")
             one_minus = 1.0 - s
             scale = one_minus[-1] / (1.0 - c.shift_terminal)
             s = (1.0 - one_minus / scale).astype(np.float32)

@@ -1,0 +1,70 @@
+"""CPU checks of the C ABI: libqie.so builds, loads, exports exactly the entry
+points include/qie.h declares with matching arity, and rejects bad arguments
+on the host (QIE_ERR_INVALID) before any GPU work -- no compute calls here."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HDR = os.path.join(ROOT, "include", "qie.h")
+
+
+def header_functions():
+    src = open(HDR).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    funcs = {}
+    for m in re.finditer(r"(?:int|const char\*)\s+(qie_\w+)\s*\(([^)]*)\)\s*;", src, flags=re.S):
+        args = [a for a in m.group(2).split(",") if a.strip() and a.strip() != "void"]
+        funcs[m.group(1)] = len(args)
+    return funcs
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from qwen_image_edit_streamdiffusion_amd import _lib
+    if not os.path.exists(_lib.LIB_PATH):
+        subprocess.run(["make", "-C", os.path.join(ROOT, "qwen_image_edit_streamdiffusion_amd", "csrc"),
+                        "-j8"], check=True, capture_output=True)
+    return _lib.load()
+
+
+def test_header_parses():
+    f = header_functions()
+    assert len(f) >= 20 and "qie_attention_fwd_bf16" in f and "qie_linear_i8" in f
+
+
+def test_every_declared_symbol_exported(lib):
+    for name in header_functions():
+        assert hasattr(lib, name), name
+
+
+def test_binding_table_matches_header(lib):
+    from qwen_image_edit_streamdiffusion_amd import _lib
+    hf = header_functions()
+    assert set(_lib.SIGNATURES) == set(hf)
+    for name, n in hf.items():
+        assert len(_lib.SIGNATURES[name]) == n, name
+
+
+def test_abi_version_and_strerror(lib):
+    assert lib.qie_abi_version() == 1
+    assert lib.qie_strerror(0) == b"ok"
+    assert b"invalid" in lib.qie_strerror(-1)
+
+
+def test_invalid_arguments_rejected_on_host(lib):
+    from qwen_image_edit_streamdiffusion_amd import _lib
+    # null pointers / bad shapes return QIE_ERR_INVALID before any launch
+    assert lib.qie_linear_bf16(None, 64, None, None, None, 64, 16, 16, 64, 0, None) == -1
+    assert lib.qie_linear_bf16(1, 64, 1, 1, 1, 64, 16, 16, 63, 0, None) == -1      # K % 64
+    assert lib.qie_gemv_bf16(16, 8, 16, 16, 16, 8, 17, 8, 8, None) == -1         # M > 16
+    kv = (ctypes.c_int * 1)(100)
+    assert lib.qie_attention_fwd_bf16(16, 1, 1, 300, kv, 16, 16, 256, 0, 0.1, None) == -1  # s_pad % 256
+    dt = (ctypes.c_float * 1)(0.5)
+    assert lib.qie_euler_step_bf16(16, 0, 16, 0, 16, 0, 17, 8, dt, None) == -1   # batch > 16
+    assert lib.qie_qk_norm_rope_bf16(16, 1, 1, 64, 256, 0, 8, 16, 16, 16, 16, 1e-6, None) == -1
+    with pytest.raises(_lib.QieError):
+        _lib.call("qie_rmsnorm_bf16", None, None, None, 1, 8, 1e-6, None)

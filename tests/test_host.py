@@ -1,0 +1,205 @@
+"""CPU checks of the product's host logic against the oracle: scheduler math,
+RoPE tables, pipeline dimension rules, diffusers state_dict packing, LoRA fuse,
+host-side argument validation, and the stream-batch slot bookkeeping (with the
+device ops replaced by CPU stand-ins, test-only)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import dit_ref as R
+from qwen_image_edit_streamdiffusion_amd import ops, pipeline, rope, scheduler, stream
+from qwen_image_edit_streamdiffusion_amd import weights as W
+from qwen_image_edit_streamdiffusion_amd.transformer import QwenImageTransformer2DModel
+
+BF16 = torch.bfloat16
+
+
+@pytest.mark.parametrize("n", [2, 3, 4, 8, 28])
+@pytest.mark.parametrize("seq", [256, 1024, 4096, 8192])
+def test_scheduler_matches_oracle(n, seq):
+    s = scheduler.FlowMatchEulerDiscreteScheduler()
+    s.set_timesteps(n, image_seq_len=seq)
+    ref, ts = R.sigma_schedule(n, seq)
+    assert torch.equal(s.sigmas, ref)
+    assert torch.equal(s.timesteps, ts)
+    for i in range(n):
+        assert s.dt(i) == float((ref[i + 1] - ref[i]).item())
+
+
+def test_scheduler_rejects_single_step_terminal_stretch():
+    with pytest.raises(ValueError):
+        scheduler.FlowMatchEulerDiscreteScheduler().set_timesteps(1, image_seq_len=4096)
+
+
+def test_model_timesteps_match_oracle():
+    ts = [1000.0, 766.7094, 455.6137, 20.0]
+    a = scheduler.model_timesteps(ts, "cpu")
+    assert torch.equal(a, R.model_timestep(torch.tensor(ts)))
+
+
+@pytest.mark.parametrize("shapes,txt", [([(1, 64, 64), (1, 64, 64)], 216), ([(1, 8, 12), (1, 16, 16)], 7),
+                                        ([(1, 32, 32)], 0)])
+def test_rope_tables_match_oracle(shapes, txt):
+    ia, ta = rope.rope_angles(shapes, txt)
+    ip, tp = R.rope_phases(shapes, txt)
+    assert torch.equal(ia, ip) and torch.equal(ta, tp)
+
+
+def test_calculate_dimensions():
+    assert pipeline.calculate_dimensions(1024 * 1024, 1.0) == (1024, 1024)
+    w, h = pipeline.calculate_dimensions(1024 * 1024, 4 / 3)
+    assert w % 32 == 0 and h % 32 == 0 and abs(w / h - 4 / 3) < 0.05
+    assert pipeline.calculate_dimensions(384 * 384, 1.0) == (384, 384)
+
+
+def _tiny_cpu_model(params=None):
+    cfg = R.tiny_config()
+    m = QwenImageTransformer2DModel(num_layers=cfg.num_layers, num_attention_heads=cfg.num_attention_heads,
+                                    joint_attention_dim=cfg.joint_attention_dim, device="cpu")
+    if params is not None:
+        m.load_diffusers_state_dict(params)
+    return cfg, m
+
+
+def test_state_dict_packing_roundtrip():
+    cfg = R.tiny_config()
+    params = R.random_params(cfg, seed=5)
+    _, m = _tiny_cpu_model(params)
+    D = cfg.inner_dim
+    blk = m.transformer_blocks[1]
+    assert torch.equal(blk.w_qkv_img[D:2 * D], params["transformer_blocks.1.attn.to_k.weight"])
+    assert torch.equal(blk.b_qkv_txt[2 * D:], params["transformer_blocks.1.attn.add_v_proj.bias"])
+    assert torch.equal(blk.w_down_txt, params["transformer_blocks.1.txt_mlp.net.2.weight"])
+    assert torch.equal(blk.norm_added_k, params["transformer_blocks.1.attn.norm_added_k.weight"])
+    out = dict(m.diffusers_state_dict())
+    assert set(out) == set(params)
+    for k, v in params.items():
+        assert torch.equal(out[k], v), k
+    assert m.config.num_layers == 2 and m.config["attention_head_dim"] == 128
+
+
+def test_state_dict_strictness():
+    cfg = R.tiny_config()
+    params = R.random_params(cfg, seed=5)
+    _, m = _tiny_cpu_model()
+    bad = dict(params)
+    bad["transformer_blocks.0.attn.bogus.weight"] = torch.zeros(1)
+    with pytest.raises(KeyError):
+        m.load_diffusers_state_dict(bad)
+    missing = dict(params)
+    missing.pop("proj_out.bias")
+    with pytest.raises(KeyError):
+        m.load_diffusers_state_dict(missing)
+
+
+def test_random_init_seeded_and_norm_weights_near_one():
+    _, a = _tiny_cpu_model()
+    _, b = _tiny_cpu_model()
+    a.random_init_(seed=7)
+    b.random_init_(seed=7)
+    for (k, x), (_, y) in zip(a.diffusers_state_dict(), b.diffusers_state_dict()):
+        assert torch.equal(x, y), k
+    nq = a.transformer_blocks[0].norm_q.float()
+    assert abs(nq.mean().item() - 1.0) < 0.02
+    assert abs(a.transformer_blocks[0].w_up_img.float().std().item() - 0.02) < 0.002
+
+
+def test_lora_fuse_on_packed_slices():
+    cfg = R.tiny_config()
+    params = R.random_params(cfg, seed=5)
+    _, m = _tiny_cpu_model(params)
+    D = cfg.inner_dim
+    g = torch.Generator().manual_seed(1)
+    A, B = torch.randn(4, D, generator=g) * 0.1, torch.randn(D, 4, generator=g) * 0.1
+    sd = {"transformer_blocks.1.attn.add_q_proj.lora_down.weight": A,
+          "transformer_blocks.1.attn.add_q_proj.lora_up.weight": B,
+          "transformer_blocks.1.attn.add_q_proj.alpha": torch.tensor(2.0),
+          "unrelated.lora_A.weight": torch.zeros(1, 1)}
+    assert W.fuse_lora(m, sd, scale=1.0) == 1
+    exp = (params["transformer_blocks.1.attn.add_q_proj.weight"].float() + 0.5 * (B @ A)).to(BF16)
+    assert torch.equal(m.transformer_blocks[1].w_qkv_txt[:D], exp)
+    # the neighbouring k slice is untouched
+    assert torch.equal(m.transformer_blocks[1].w_qkv_txt[D:2 * D],
+                       params["transformer_blocks.1.attn.add_k_proj.weight"])
+
+
+def test_ops_reject_host_tensors():
+    x = torch.zeros(32, 64, dtype=BF16)
+    with pytest.raises(ValueError):
+        ops.linear(x, torch.zeros(64, 64, dtype=BF16), torch.zeros(64, dtype=BF16))
+    with pytest.raises(ValueError):
+        ops.silu(x)
+
+
+def test_flops_match_oracle():
+    from qwen_image_edit_streamdiffusion_amd.transformer import TransformerConfig
+    full = QwenImageTransformer2DModel.__new__(QwenImageTransformer2DModel)  # no 41 GB allocation
+    full.config = TransformerConfig()
+    assert QwenImageTransformer2DModel.flops_per_forward(full, 8192, 216) == pytest.approx(
+        R.flops_per_forward(8192, 216))
+
+
+# ----------------------------------------------------------------------------- stream bookkeeping
+class _FakeTF:
+    """Deterministic per-row stand-in for the DiT: v = 0.5*x + t (row-local)."""
+    device = torch.device("cpu")
+
+    def __call__(self, inp, enc, mask, t, shapes, lens, return_dict=False):
+        return (0.5 * inp.float() + t.float()[:, None, None]).to(BF16),
+
+
+@pytest.fixture
+def cpu_ops(monkeypatch):
+    def copy_batched(src, dst):
+        dst.copy_(src)
+        return dst
+
+    def euler_step(x, v, dt, out):
+        for b in range(x.shape[0]):
+            out[b] = R.euler_step(x[b], v[b], 0.0, dt[b])
+        return out
+
+    def cfg_combine(c, u, s, out=None):
+        r = R.cfg_combine(c, u, s)
+        if out is not None:
+            out.copy_(r)
+            return out
+        return r
+
+    monkeypatch.setattr(stream.ops, "copy_batched", copy_batched)
+    monkeypatch.setattr(stream.ops, "euler_step", euler_step)
+    monkeypatch.setattr(stream.ops, "cfg_combine", cfg_combine)
+
+
+def _serial(tf, noise, cond, steps, cfg_scale, pe, ne):
+    eng = stream.StreamBatchDenoiser(tf, num_steps=steps, true_cfg_scale=cfg_scale, latent_hw=(2, 2),
+                                     cond_hw=(2, 2))
+    eng.set_conditions(pe, None, ne)
+    eng.push(noise, cond)
+    return eng.flush()[0][1]
+
+
+@pytest.mark.parametrize("steps,cfg_scale", [(2, 1.0), (3, 1.0), (2, 4.0)])
+def test_stream_slots_fill_steady_flush(cpu_ops, steps, cfg_scale):
+    tf = _FakeTF()
+    pe = torch.randn(1, 5, 8).to(BF16)
+    ne = torch.randn(1, 3, 8).to(BF16) if cfg_scale > 1 else None
+    eng = stream.StreamBatchDenoiser(tf, num_steps=steps, true_cfg_scale=cfg_scale, latent_hw=(2, 2),
+                                     cond_hw=(2, 2))
+    eng.set_conditions(pe, None, ne)
+    g = torch.Generator().manual_seed(0)
+    frames = [(torch.randn(1, 4, 64, generator=g).to(BF16), torch.randn(1, 4, 64, generator=g).to(BF16))
+              for _ in range(6)]
+    got = []
+    for i, (n, c) in enumerate(frames):
+        r = eng.push(n, c)
+        if i < steps - 1:
+            assert r is None  # pipeline filling
+        else:
+            assert r is not None and r[0] == i - steps + 1  # FIFO, one frame per push
+            got.append(r)
+    got += eng.flush()
+    assert [f for f, _ in got] == list(range(6))
+    for fid, lat in got:
+        ref = _serial(tf, frames[fid][0], frames[fid][1], steps, cfg_scale, pe, ne)
+        assert torch.equal(lat, ref), fid
