@@ -78,7 +78,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="stream2", choices=["stream2", "stream2-int8", "cfg4"])
+    ap.add_argument("--workload", default="stream2", choices=["stream2", "stream2-int8", "stream2-cfg", "cfg4"])
     ap.add_argument("--layers", type=int, default=60, help="debug only; the headline needs 60")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-probe", action="store_true")
@@ -114,10 +114,15 @@ def main():
 
     probe_keys = ("attention", "mlp_up")
     if args.workload.startswith("stream2"):
-        eng = StreamBatchDenoiser(model, num_steps=2, true_cfg_scale=1.0, latent_hw=(64, 64),
-                                  cond_hw=(64, 64))
-        eng.set_conditions(pe)
-        rows = 2
+        cfg_on = args.workload == "stream2-cfg"
+        eng = StreamBatchDenoiser(model, num_steps=2, true_cfg_scale=4.0 if cfg_on else 1.0,
+                                  latent_hw=(64, 64), cond_hw=(64, 64))
+        if cfg_on:  # true CFG 4.0 with a shorter negative prompt: cond + uncond rows, B = 4
+            ne = torch.randn(1, 211, 3584, generator=g, device=dev, dtype=BF16)
+            eng.set_conditions(pe, None, ne)
+        else:
+            eng.set_conditions(pe)
+        rows = 4 if cfg_on else 2
         fwd_per_step = 1
 
         def step(i):
@@ -200,8 +205,15 @@ def main():
         dom = max(kernels, key=lambda k: kernels[k]["total_ms"])
         kd = kernels[dom]
         kpeak = PEAK_BF16 if dom == "attention" else peak
+        # HBM bytes per launch of this kernel from the committed rocprofv3 FETCH_SIZE /
+        # WRITE_SIZE passes (tools/measure.sh + tools/summarize_profile.py), if present
+        traffic = None
+        tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        if os.path.exists(tf) and args.workload == "stream2":
+            t = json.load(open(tf)).get("traffic_per_launch", {}).get(dom)
+            traffic = t and t.get("hbm_bytes_per_launch")
         roof = {"bound": "mfma", "kernel": dom, "achieved": kd["tflops"], "peak": kpeak / 1e12,
-                "unit": "TFLOP/s", "frac": kd["frac"], "traffic": None,
+                "unit": "TFLOP/s", "frac": kd["frac"], "traffic": traffic,
                 "flops_per_launch": (4.0 * rows * S * S * 3072 if dom == "attention"
                                      else 2.0 * rows * (S_NOISE + S_COND) * 12288 * 3072),
                 "avg_launch_ms": kd["avg_ms"]}
@@ -217,6 +229,7 @@ def main():
         workload = {"stream2": "lightning-2step stream-batch depth=2, cond-only, 1024x1024 (configs[2])",
                     "stream2-int8": "int8 W8A8 linears, lightning-2step stream-batch depth=2, 1024x1024 "
                                     "(configs[3])",
+                    "stream2-cfg": "lightning-2step stream-batch depth=2 + true-CFG 4.0 (B=4), 1024x1024",
                     "cfg4": "4-step true-CFG 4.0 batched cond/uncond, 1024x1024 (configs[1])"}[args.workload]
         line = {
             "metric": "images/sec, 1024x1024 2-step Lightning edit (DiT denoise)",

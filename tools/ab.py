@@ -1,0 +1,90 @@
+#!/usr/bin/env python3
+"""Same-process A/B of two builds of a libqie kernel (cdna_hip_programming.md
+§5.4 rule 24: interleaved rounds in ONE process, report median and min).
+
+    python tools/ab.py attention path/to/libA.so path/to/libB.so [rounds]
+
+Both libraries are loaded side by side with ctypes; launches alternate A, B, A,
+B ... on the same random inputs (headline shape B=2, S=8408)."""
+import ctypes
+import math
+import statistics
+import sys
+
+import torch
+
+BF16 = torch.bfloat16
+
+
+def load(path):
+    lib = ctypes.CDLL(path)
+    lib.qie_attention_fwd_bf16.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                           ctypes.POINTER(ctypes.c_int), ctypes.c_void_p, ctypes.c_void_p,
+                                           ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_void_p]
+    lib.qie_linear_bf16.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
+                                    ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                    ctypes.c_int, ctypes.c_void_p]
+    return lib
+
+
+def main():
+    what, pa, pb = sys.argv[1:4]
+    rounds = int(sys.argv[4]) if len(sys.argv) > 4 else 10
+    libs = [load(pa), load(pb)]
+    dev = torch.device("cuda:0")
+    st = torch.cuda.current_stream().cuda_stream
+    if what == "attention":
+        B, H, S_IMG, S_TXT = 2, 24, 8192, 216
+        S = S_IMG + S_TXT
+        s_pad = ((S + 255) // 256) * 256
+        qkv = torch.randn(3, B, H, s_pad, 128, device=dev).to(BF16)
+        qkv[:, :, :, S:] = 0
+        outs = [(torch.empty(B * S_IMG, H * 128, dtype=BF16, device=dev),
+                 torch.empty(B * S_TXT, H * 128, dtype=BF16, device=dev)) for _ in libs]
+        kv = (ctypes.c_int * B)(*[S] * B)
+        flops = 4.0 * B * S * S * H * 128
+
+        def run(i):
+            rc = libs[i].qie_attention_fwd_bf16(qkv.data_ptr(), B, H, s_pad, kv, outs[i][0].data_ptr(),
+                                                outs[i][1].data_ptr(), S_IMG, S_TXT, 1 / math.sqrt(128), st)
+            assert rc == 0, rc
+    elif what.startswith("gemm"):
+        M, N, K = {"gemm_up": (16384, 12288, 3072), "gemm_qkv": (16384, 9216, 3072),
+                   "gemm_down": (16384, 3072, 12288)}[what]
+        x = torch.randn(M, K, device=dev).to(BF16)
+        w = (torch.randn(N, K, device=dev) * 0.02).to(BF16)
+        b = torch.zeros(N, device=dev, dtype=BF16)
+        outs = [torch.empty(M, N, dtype=BF16, device=dev) for _ in libs]
+        flops = 2.0 * M * N * K
+
+        def run(i):
+            rc = libs[i].qie_linear_bf16(x.data_ptr(), K, w.data_ptr(), b.data_ptr(), outs[i].data_ptr(), N,
+                                         M, N, K, 0, st)
+            assert rc == 0, rc
+    else:
+        raise SystemExit(f"unknown kernel {what}")
+    times = [[], []]
+    for _ in range(3):
+        run(0)
+        run(1)
+    torch.cuda.synchronize()
+    for _ in range(rounds):
+        for i in (0, 1):
+            a, bb = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            for _ in range(5):
+                run(i)
+            bb.record()
+            torch.cuda.synchronize()
+            times[i].append(a.elapsed_time(bb) / 5)
+    o0 = outs[0][0] if isinstance(outs[0], tuple) else outs[0]
+    o1 = outs[1][0] if isinstance(outs[1], tuple) else outs[1]
+    diff = (o0.float() - o1.float()).abs().max().item()
+    for i, name in enumerate(("A", "B")):
+        med, mn = statistics.median(times[i]), min(times[i])
+        print(f"{what} {name}: median {med:.3f} ms  min {mn:.3f} ms  {flops / med / 1e9:.0f} TFLOP/s")
+    print(f"max |A-B| = {diff:.3e}")
+
+
+if __name__ == "__main__":
+    main()

@@ -102,6 +102,15 @@ def bench_misc():
 
 
 def main():
+    if len(sys.argv) > 2 and sys.argv[1] == "one":  # single kernel, for rocprofv3 --pmc passes
+        M = B * S_IMG
+        shapes = {"mlp_up_plain": (M, F, D, "plain"), "mlp_down_gate": (M, D, F, "gate"),
+                  "qkv": (M, 3 * D, D, "qkv"), "out_gate": (M, D, D, "gate")}
+        if sys.argv[2] == "attention":
+            print(bench_attention())
+        else:
+            print(bench_gemm(sys.argv[2], *shapes[sys.argv[2]]))
+        return
     want = set(sys.argv[1:])
     res = []
     if not want or "attention" in want:
