@@ -4,19 +4,23 @@
 // QwenImageTransformerBlock [U] -- the 68.7 %
 // of DiT FLOPs that are linear.
 //
-// Design (gfx950, cdna_hip_programming.md §5):
-//   * both operands are K-contiguous (activation rows, nn.Linear weight rows),
-//     staged global -> LDS with 16-byte global_load_lds (LDS-DMA), one 128-byte
-//     K-row per tile row (BK = 64 bf16 or 128 int8), double buffered;
-//   * LDS image XOR-swizzled at 16-byte granularity, chunk' = chunk ^ ((row>>1)&7):
-//     the 16-lane ds_read_b128 groups of the MFMA operand reads are conflict-free;
-//     the swizzle is applied on the per-lane GLOBAL address (LDS-DMA writes are
-//     lane-linear, rule 21);
-//   * MFMA 16x16x32 bf16 (or 16x16x64 i8) with the WEIGHT tile as the A operand
-//     and the activation tile as B, so each lane ends up owning 4 consecutive
-//     output columns of one row -> 8-byte epilogue stores;
-//   * XCD-aware bijective block remap + grouped tile order so the 32 CUs of one
-//     XCD work on a compact block of tiles (L2 reuse).
+// Two kernels, both gfx950-only (cdna_hip_programming.md §5):
+//   gemm_ring_kernel (big shapes: M, N >= 256, >= 160 tiles, aligned output) -- 256x256 tile,
+//     8 waves, 4-slot LDS ring of 32-wide K slices fed by buffer_load...lds three slices ahead,
+//     fragments of slice k+1 read into registers during slice k, asm MFMAs with in-place
+//     accumulators, permlane16-widened 16-byte epilogue stores. See its section below.
+//   gemm_kernel (everything else: text-stream rows, small N) -- BMxBN tile, 2-stage:
+//     * both operands are K-contiguous (activation rows, nn.Linear weight rows),
+//       staged global -> LDS with 16-byte global_load_lds (LDS-DMA), one 128-byte
+//       K-row per tile row (BK = 64 bf16 or 128 int8), double buffered;
+//     * LDS image XOR-swizzled at 16-byte granularity, chunk' = chunk ^ ((row>>1)&7):
+//       conflict-free for the ds_read_b128 lane groups; the swizzle is applied on the
+//       per-lane GLOBAL address (LDS-DMA writes are lane-linear, rule 21);
+// Common: MFMA 16x16x32 bf16 (or 16x16x64 i8) with the WEIGHT tile as the A operand and the
+// activation tile as B, so each lane owns 4 consecutive output columns of one row; XCD-aware
+// bijective block remap + grouped tile order so the 32 CUs of one XCD share L2-resident tiles.
+#include <type_traits>
+
 #include "qie_common.h"
 
 namespace {
@@ -135,6 +139,64 @@ __device__ __forceinline__ void epilogue4(const EpiArgs& e, int m, int n, const 
   }
 }
 
+// ---- wide epilogue (gemm_ring): lanes of one 16x16 MFMA tile hold 4 consecutive columns of one
+// row (column group g = lane>>4). One v_permlane16_swap per dword between tiles j and j+1 gives
+// every lane 8 consecutive columns: g0 <- tile j cols 0-7, g1 <- tile j+1 cols 0-7, g2 <- tile j
+// cols 8-15, g3 <- tile j+1 cols 8-15 -> one 16-byte store per lane per tile pair, 64 contiguous
+// bytes per row (cdna_hip_programming.md T21, adapted from permlane32 to the 16x16 layout).
+// Pre-swap part: bias (+ int8 scales), bf16 rounding, activation, packed to 4 bf16.
+template <int EPI, bool I8>
+__device__ __forceinline__ u32x2_t epi_pre(const EpiArgs& e, int m, int n,
+                                           const typename MfmaOp<I8>::acc& a) {
+  const u32x2_t bw = *(const u32x2_t*)(e.bias + n);
+  const float b4[4] = {lo_f(bw.x), hi_f(bw.x), lo_f(bw.y), hi_f(bw.y)};
+  float v[4];
+  if constexpr (I8) {
+    const float sx = e.sx[m];
+    const f32x4_t sw = *(const f32x4_t*)(e.sw + n);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = rbf(__builtin_fmaf((float)a[j], sx * sw[j], b4[j]));
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = rbf(a[j] + b4[j]);
+  }
+  if constexpr (EPI == EPI_GELU) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = gelu_tanh_f(v[j]);
+  }
+  return u32x2_t{pack2(v[0], v[1]), pack2(v[2], v[3])};
+}
+
+// Post-swap part: 8 consecutive bf16 columns n..n+7 of row m (16-byte aligned, host-checked).
+template <int EPI>
+__device__ __forceinline__ void epi_store8(const EpiArgs& e, int m, int n, u32x4_t v) {
+  if constexpr (EPI == EPI_BIAS || EPI == EPI_GELU) {
+    *(u32x4_t*)((bf16_t*)e.out + (int64_t)m * e.ldo + n) = v;
+  } else if constexpr (EPI == EPI_GATE_RES) {
+    const int b = m / e.rows_per_batch;
+    const u32x4_t gw = *(const u32x4_t*)(e.gate + (int64_t)b * e.gate_bstride + n);
+    bf16_t* x = (bf16_t*)e.out + (int64_t)m * e.ldo + n;
+    const u32x4_t xw = *(const u32x4_t*)x;
+    const uint32_t vv[4] = {v.x, v.y, v.z, v.w}, gg[4] = {gw.x, gw.y, gw.z, gw.w},
+                   xx[4] = {xw.x, xw.y, xw.z, xw.w};
+    uint32_t o[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      o[k] = pack2(lo_f(xx[k]) + rbf(lo_f(gg[k]) * lo_f(vv[k])), hi_f(xx[k]) + rbf(hi_f(gg[k]) * hi_f(vv[k])));
+    *(u32x4_t*)x = u32x4_t{o[0], o[1], o[2], o[3]};
+  } else {  // EPI_QKV: 8 columns stay inside one head (head_dim % 8 == 0)
+    const int hd = e.heads * e.head_dim;
+    const int which = n / hd;
+    const int hn = n - which * hd;
+    const int h = hn / e.head_dim;
+    const int d = hn - h * e.head_dim;
+    const int b = m / e.rows_per_batch;
+    const int s = e.seq_offset + (m - b * e.rows_per_batch);
+    const int64_t off = ((((int64_t)which * e.batch + b) * e.heads + h) * e.s_pad + s) * e.head_dim + d;
+    *(u32x4_t*)((bf16_t*)e.out + off) = v;
+  }
+}
+
 template <int BM, int BN, int WM, int WN, int EPI, bool I8>
 __global__ void __launch_bounds__(WM* WN * 64)
     gemm_kernel(const char* __restrict__ X, int64_t ldx_b, const char* __restrict__ W, int64_t ldw_b,
@@ -234,6 +296,221 @@ __global__ void __launch_bounds__(WM* WN * 64)
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// gemm_ring: 256x256 block tile; NT=4: 8 waves (2 per SIMD) of 128x64, NT=8: 4 waves of 128x128
+// (8x8 MFMA 16x16 tiles = 256 accumulator registers = the whole AGPR half of the file).
+//   * K advances in 64-byte slices (32 bf16 / 64 int8 = one MFMA K-step) through a 4-slot
+//     LDS ring filled by LDS-DMA (buffer_load ... lds) three slices ahead;
+//   * the fragments of slice k+1 are read into the second register set while the 64 MFMAs of
+//     slice k run: after every 4th MFMA one ds_read_b128, after every 8th one 1-KiB DMA piece,
+//     so LDS latency is covered by the wave's own MFMA stream instead of a second wave;
+//   * the MFMAs are inline asm with the accumulator tied in place ("+a"): the 256 accumulators
+//     exactly fill the AGPRs and hipcc's allocator otherwise rotates them through VGPR copies;
+//     being volatile they also pin the interleave above (hipcc keeps memory ops in order
+//     around them) -- the waits for the fragment reads are still hipcc's own (lgkmcnt);
+//   * one barrier per slice, counted vmcnt(8) keeps the newest slice in flight.
+// LDS rows are 64 B (4 x 16-byte chunks); chunk' = chunk ^ 3*((row>>3)&1) is conflict-free for
+// the ds_read_b128 lane groups {0-3,12-15,20-27} / {4-11,16-19,28-31} (MI355X_MICROARCH §LDS)
+// of the 16-row fragment read.
+constexpr int k4RowBytes = 64;
+constexpr int k4Tile = 256 * k4RowBytes;  // one operand slice, 16 KiB
+constexpr int k4Stage = 2 * k4Tile;       // X + W slice, 32 KiB
+constexpr int k4Slots = 4;
+// 4 = the 8-wave form (measured +3..7.5 % over the 2-stage kernel on the DiT GEMMs, bitwise equal);
+// 8 = the 4-wave form, 5 % slower: one wave per SIMD exposes each LDS-DMA piece's issue cost
+constexpr int kRingNT = 4;
+
+__device__ __forceinline__ int swz4(int row) { return ((row >> 3) & 1) * 3; }
+
+// per-lane byte offsets of the PPW 1-KiB pieces a wave stages per operand slice
+template <int NWAVE>
+__device__ __forceinline__ void stage4_offsets(int64_t ld_bytes, int rows_valid, int wave, int lane,
+                                               uint32_t* off) {
+#pragma unroll
+  for (int i = 0; i < 16 / NWAVE; ++i) {
+    const int r = (wave + i * NWAVE) * 16 + (lane >> 2);  // 16 rows (1 KiB) per wave-instruction
+    const int c = (lane & 3) ^ swz4(r);
+    const int gr = r < rows_valid ? r : rows_valid - 1;
+    off[i] = (uint32_t)(gr * ld_bytes) + (c << 4);
+  }
+}
+
+// buffer descriptor over [base, base + bytes) (wave-uniform inputs only); kept out of the kernel
+// body so the host pass, which has no AMDGPU builtin types, still emits the launch stub
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const char* base, int bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, bytes, 0x00020000);
+}
+__device__ __forceinline__ void dma_piece(const __amdgpu_buffer_rsrc_t& r, char QIE_LDS* dst, uint32_t voff,
+                                          int soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (QIE_LDS void*)dst, 16, voff, soff, 0, 0);
+}
+
+template <bool I8>
+struct Mma4;
+template <>
+struct Mma4<false> {
+  static __device__ __forceinline__ void acc(f32x4_t& c, const bf16x8_t& a, const bf16x8_t& b) {
+    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
+  }
+  static __device__ __forceinline__ void init(f32x4_t& c, const bf16x8_t& a, const bf16x8_t& b) {
+    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(c) : "v"(a), "v"(b));
+  }
+};
+template <>
+struct Mma4<true> {
+  static __device__ __forceinline__ void acc(i32x4_t& c, const i32x4_t& a, const i32x4_t& b) {
+    asm volatile("v_mfma_i32_16x16x64_i8 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
+  }
+  static __device__ __forceinline__ void init(i32x4_t& c, const i32x4_t& a, const i32x4_t& b) {
+    asm volatile("v_mfma_i32_16x16x64_i8 %0, %1, %2, 0" : "=a"(c) : "v"(a), "v"(b));
+  }
+};
+
+// NT = 16-column MFMA tiles per wave: 8 -> 4 waves (2x2, 128x128 per wave, one wave per SIMD);
+// 4 -> 8 waves (2x4, 128x64 per wave, two per SIMD: a wave's DMA issue hides behind its partner)
+template <int NT, int EPI, bool I8>
+__global__ void __launch_bounds__(NT == 8 ? 256 : 512, 1)
+    gemm_ring_kernel(const char* __restrict__ X, int64_t ldx_b, const char* __restrict__ W, int64_t ldw_b,
+                  int M, int N, int K_bytes, EpiArgs e) {
+  using frag = typename MfmaOp<I8>::frag;
+  using accT = typename MfmaOp<I8>::acc;
+  __shared__ __attribute__((aligned(16))) char smem_raw[k4Slots * k4Stage];
+  char QIE_LDS* smem = (char QIE_LDS*)smem_raw;
+
+  const int tiles_m = (M + 255) >> 8, tiles_n = (N + 255) >> 8;
+  const int nwg = tiles_m * tiles_n;
+  const int wgid = xcd_remap(blockIdx.x, nwg);
+  constexpr int GROUP = 8;
+  const int per_group = GROUP * tiles_n;
+  const int first_m = (wgid / per_group) * GROUP;
+  const int gsz = min(tiles_m - first_m, GROUP);
+  const int tm = first_m + (wgid % per_group) % gsz;
+  const int tn = (wgid % per_group) / gsz;
+  const int m0 = tm * 256, n0 = tn * 256;
+
+  constexpr int WN = 256 / (NT * 16), NWAVE = 2 * WN, PPW = 16 / NWAVE;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int wm = wave / WN, wn = wave % WN;
+  const int m_valid = M - m0, n_valid = N - n0;
+  const int nk = K_bytes / k4RowBytes;  // host guarantees nk >= 4
+
+  // buffer descriptors over this block's operand rows (wave-uniform); per-lane row offsets in
+  // 32-bit VGPRs, the K position in the scalar offset
+  const auto xr = make_rsrc(X + (int64_t)m0 * ldx_b, (int)(min(m_valid, 256) * ldx_b));
+  const auto wr = make_rsrc(W + (int64_t)n0 * ldw_b, (int)(min(n_valid, 256) * ldw_b));
+  uint32_t xo[PPW], wo[PPW];
+  stage4_offsets<NWAVE>(ldx_b, m_valid, wave, lane, xo);
+  stage4_offsets<NWAVE>(ldw_b, n_valid, wave, lane, wo);
+  // DMA piece p (0..2*PPW-1) of slice kt: p < PPW -> X rows, else W rows
+  auto dma = [&](int kt, int p) {
+    const bool isw = p >= PPW;
+    const int pi = isw ? p - PPW : p;
+    char QIE_LDS* dst = smem + (kt & (k4Slots - 1)) * k4Stage + (isw ? k4Tile : 0) +
+                        (wave + pi * NWAVE) * 1024;
+    if (isw) dma_piece(wr, dst, wo[pi], kt * k4RowBytes);
+    else dma_piece(xr, dst, xo[pi], kt * k4RowBytes);
+  };
+
+  // fragment r of a slice: r < 8 -> W rows wn*16*NT + 16r + fr, else X rows wm*128 + 16(r-8) + fr
+  const int fr = lane & 15;
+  const int cofs = ((lane >> 4) ^ swz4(fr)) << 4;
+  const int a_off = (wm * 128 + fr) * k4RowBytes + cofs;
+  const int w_off = k4Tile + (wn * NT * 16 + fr) * k4RowBytes + cofs;
+  auto ldfrag = [&](int kt, int r) -> frag {
+    const char QIE_LDS* base = smem + (kt & (k4Slots - 1)) * k4Stage;
+    return *(const frag QIE_LDS*)(base + (r < 8 ? w_off + r * 16 * k4RowBytes
+                                                 : a_off + (r - 8) * 16 * k4RowBytes));
+  };
+
+  accT acc[8][NT];
+  frag af[2][8], wf[2][NT];
+
+  // slice kt: 64 MFMAs on register set CUR; interleaved reads of slice kt+1 into set CUR^1 and
+  // DMA of slice kt+3 into the slot last read by slice kt-2 (consumed before this barrier)
+  auto slice = [&](auto cur_t, auto init_t, auto read_t, auto dma_t, auto wait8_t, int kt) {
+    constexpr int CUR = decltype(cur_t)::value;
+    constexpr bool INIT = decltype(init_t)::value, READ = decltype(read_t)::value;
+    constexpr bool DMA = decltype(dma_t)::value, WAIT8 = decltype(wait8_t)::value;
+    if constexpr (READ) {  // slice kt+1 landed: one slice (2*PPW pieces) may stay in flight
+      if constexpr (!WAIT8) asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+      else if constexpr (PPW == 4) asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
+    }
+#pragma unroll
+    for (int q = 0; q < 8 * NT; ++q) {
+      const int i = q / NT, j = q % NT;
+      if constexpr (INIT) Mma4<I8>::init(acc[i][j], wf[CUR][j], af[CUR][i]);
+      else Mma4<I8>::acc(acc[i][j], wf[CUR][j], af[CUR][i]);
+      if constexpr (READ) {
+        // W fragments of slice kt+1 early (row 0 of the next slice needs all 8); the A
+        // fragment of row i right after row i's last MFMA, so it can reuse row i's registers
+        if ((q & 3) == 1 && q < 4 * NT) wf[CUR ^ 1][q >> 2] = ldfrag(kt + 1, q >> 2);
+        if (j == NT - 1) af[CUR ^ 1][i] = ldfrag(kt + 1, 8 + i);
+      }
+      if constexpr (DMA) {
+        if ((q & 7) == 3) dma(kt + 3, q >> 3);
+      }
+    }
+  };
+  using T = std::true_type;
+  using F = std::false_type;
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+
+  // prologue: slices 0..2 in flight, slice 0 landed, its fragments read
+#pragma unroll
+  for (int p = 0; p < 2 * PPW; ++p) dma(0, p);
+#pragma unroll
+  for (int p = 0; p < 2 * PPW; ++p) dma(1, p);
+#pragma unroll
+  for (int p = 0; p < 2 * PPW; ++p) dma(2, p);
+  if constexpr (PPW == 4) asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
+#pragma unroll
+  for (int r = 0; r < NT; ++r) wf[0][r] = ldfrag(0, r);
+#pragma unroll
+  for (int r = 0; r < 8; ++r) af[0][r] = ldfrag(0, 8 + r);
+  slice(I0{}, T{}, T{}, T{}, T{}, 0);  // slice 0 (nk >= 4: slice 3 exists)
+  int kt = 1;
+  for (; kt + 4 < nk; kt += 2) {  // steady state: slices kt, kt+1 both stage kt+3 / kt+4
+    slice(I1{}, F{}, T{}, T{}, T{}, kt);
+    slice(I0{}, F{}, T{}, T{}, T{}, kt + 1);
+  }
+  // tail: nk is even (host: K_bytes % 128 == 0), so the loop leaves exactly slices
+  // nk-3 .. nk-1, register set 1 first (a data-dependent branch here makes hipcc spill AGPRs)
+  slice(I1{}, F{}, T{}, F{}, T{}, kt);      // reads nk-2, everything staged
+  slice(I0{}, F{}, T{}, F{}, F{}, kt + 1);  // reads nk-1: vmcnt(0)
+  slice(I1{}, F{}, F{}, F{}, F{}, kt + 2);
+  // MFMA D -> VALU read hazard for the last row of accumulators (asm is not padded by hipcc)
+  if constexpr (NT == 8)
+    asm volatile("s_nop 15\n\ts_nop 7"
+                 : "+a"(acc[7][0]), "+a"(acc[7][1]), "+a"(acc[7][2]), "+a"(acc[7][3]), "+a"(acc[7][4]),
+                   "+a"(acc[7][5]), "+a"(acc[7][NT - 2]), "+a"(acc[7][NT - 1]));
+  else
+    asm volatile("s_nop 15\n\ts_nop 7"
+                 : "+a"(acc[7][0]), "+a"(acc[7][1]), "+a"(acc[7][2]), "+a"(acc[7][3]), "+a"(acc[6][0]),
+                   "+a"(acc[6][1]), "+a"(acc[6][2]), "+a"(acc[6][NT - 1]));
+
+  // wide epilogue; every lane takes part in the swaps, rows/columns past M/N are clamped for the
+  // loads and skipped for the store (N % 8 == 0, host-checked)
+  const int g = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int m = m0 + wm * 128 + i * 16 + fr;
+    const int mc = min(m, M - 1);
+#pragma unroll
+    for (int jp = 0; jp < NT / 2; ++jp) {
+      const int nb = n0 + wn * NT * 16 + jp * 32;
+      u32x2_t a = epi_pre<EPI, I8>(e, mc, min(nb + g * 4, N - 4), acc[i][2 * jp]);
+      u32x2_t b = epi_pre<EPI, I8>(e, mc, min(nb + 16 + g * 4, N - 4), acc[i][2 * jp + 1]);
+      const auto sx = __builtin_amdgcn_permlane16_swap(a.x, b.x, false, false);
+      const auto sy = __builtin_amdgcn_permlane16_swap(a.y, b.y, false, false);
+      const int n = nb + (g & 1) * 16 + (g >> 1) * 8;
+      if (m < M && n < N) epi_store8<EPI>(e, m, n, u32x4_t{sx[0], sy[0], sx[1], sy[1]});
+    }
+  }
+}
+
 template <int EPI, bool I8>
 int launch_gemm(const void* x, int64_t ldx, const void* w, int64_t ldw, int M, int N, int K,
                 const EpiArgs& e, hipStream_t s) {
@@ -246,6 +523,14 @@ int launch_gemm(const void* x, int64_t ldx, const void* w, int64_t ldw, int M, i
   const int64_t ldx_b = ldx * eb, ldw_b = ldw * eb;
   const int kb = K * eb;
   const int64_t big_tiles = (int64_t)((M + 255) / 256) * ((N + 255) / 256);
+  const bool wide = N % 8 == 0 && ((uintptr_t)e.out % 16) == 0 && e.ldo % 8 == 0 &&
+                    (EPI != EPI_GATE_RES || (((uintptr_t)e.gate % 16) == 0 && e.gate_bstride % 8 == 0)) &&
+                    (EPI != EPI_QKV || e.head_dim % 8 == 0);
+  if (wide && M >= 256 && N >= 256 && big_tiles >= 160 && kb >= 4 * k4RowBytes) {
+    gemm_ring_kernel<kRingNT, EPI, I8><<<(int)big_tiles, 2 * (256 / (kRingNT * 16)) * 64, 0, s>>>((const char*)x, ldx_b, (const char*)w, ldw_b,
+                                                         M, N, kb, e);
+    return qie_last_error();
+  }
   if (M >= 256 && N >= 256 && big_tiles >= 160) {
     const int nwg = (int)big_tiles;
     gemm_kernel<256, 256, 2, 4, EPI, I8><<<nwg, 512, 0, s>>>((const char*)x, ldx_b, (const char*)w,

@@ -2,10 +2,10 @@
 """Same-process A/B of two builds of a libqie kernel (cdna_hip_programming.md
 §5.4 rule 24: interleaved rounds in ONE process, report median and min).
 
-    python tools/ab.py attention path/to/libA.so path/to/libB.so [rounds]
+    python tools/ab.py attention path/to/libA.so path/to/libB.so [more.so ...] [rounds]
 
-Both libraries are loaded side by side with ctypes; launches alternate A, B, A,
-B ... on the same random inputs (headline shape B=2, S=8408)."""
+All libraries are loaded side by side with ctypes; launches alternate A, B, C, A, B, C ...
+on the same random inputs (headline shapes: attention B=2, S=8408; the three DiT GEMMs)."""
 import ctypes
 import math
 import statistics
@@ -28,9 +28,11 @@ def load(path):
 
 
 def main():
-    what, pa, pb = sys.argv[1:4]
-    rounds = int(sys.argv[4]) if len(sys.argv) > 4 else 10
-    libs = [load(pa), load(pb)]
+    what = sys.argv[1]
+    paths = [a for a in sys.argv[2:] if a.endswith(".so")]
+    rest = [a for a in sys.argv[2:] if not a.endswith(".so")]
+    rounds = int(rest[0]) if rest else 10
+    libs = [load(p) for p in paths]
     dev = torch.device("cuda:0")
     st = torch.cuda.current_stream().cuda_stream
     if what == "attention":
@@ -63,13 +65,14 @@ def main():
             assert rc == 0, rc
     else:
         raise SystemExit(f"unknown kernel {what}")
-    times = [[], []]
+    L = len(libs)
+    times = [[] for _ in range(L)]
     for _ in range(3):
-        run(0)
-        run(1)
+        for i in range(L):
+            run(i)
     torch.cuda.synchronize()
     for _ in range(rounds):
-        for i in (0, 1):
+        for i in range(L):
             a, bb = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record()
             for _ in range(5):
@@ -77,13 +80,12 @@ def main():
             bb.record()
             torch.cuda.synchronize()
             times[i].append(a.elapsed_time(bb) / 5)
-    o0 = outs[0][0] if isinstance(outs[0], tuple) else outs[0]
-    o1 = outs[1][0] if isinstance(outs[1], tuple) else outs[1]
-    diff = (o0.float() - o1.float()).abs().max().item()
-    for i, name in enumerate(("A", "B")):
+    first = [o[0] if isinstance(o, tuple) else o for o in outs]
+    for i in range(L):
         med, mn = statistics.median(times[i]), min(times[i])
-        print(f"{what} {name}: median {med:.3f} ms  min {mn:.3f} ms  {flops / med / 1e9:.0f} TFLOP/s")
-    print(f"max |A-B| = {diff:.3e}")
+        diff = (first[0].float() - first[i].float()).abs().max().item()
+        print(f"{what} {paths[i]}: median {med:.3f} ms  min {mn:.3f} ms  {flops / med / 1e9:.0f} TFLOP/s"
+              f"  max|diff vs first| {diff:.3e}")
 
 
 if __name__ == "__main__":

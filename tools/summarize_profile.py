@@ -21,8 +21,8 @@ import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KEYS = {"attention": "attn_fwd_kernel", "mlp_up": "gemm_kernel<256, 256, 2, 4, 1, false>",
-        "gated_gemm": "gemm_kernel<256, 256, 2, 4, 2, false>", "qkv_gemm": "gemm_kernel<256, 256, 2, 4, 3, false>"}
+KEYS = {"attention": "attn_fwd_kernel", "mlp_up": "gemm_ring_kernel<4, 1, false>",
+        "gated_gemm": "gemm_ring_kernel<4, 2, false>", "qkv_gemm": "gemm_ring_kernel<4, 3, false>"}
 
 
 def main():
