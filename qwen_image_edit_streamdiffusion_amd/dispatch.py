@@ -1,0 +1,134 @@
+"""Multi-GPU request dispatcher for the ``/edit`` server.
+
+The reference serves one request at a time on one pinned GPU (``CUDA_VISIBLE_DEVICES='7'``,
+one-thread executor, 429 while busy: server.py:8, 39-40, 190-191). Here one worker process per
+GPU owns its own pipeline, and the server hands each request to any idle worker. It answers 429
+only when every worker is busy. Requests are independent, so nothing is exchanged between
+GPUs (the multi-GPU axis of SURVEY.md §8 e, "frames / requests round-robin").
+
+Workers are started with the ``spawn`` method before the server process touches the GPU.
+``start()`` refuses to run if this process has already initialised HIP: spawning re-executes
+the interpreter, and exec from a GPU-initialised process is unsafe on this platform.
+Images cross the process boundary as PNG bytes.
+"""
+from __future__ import annotations
+
+import io
+import multiprocessing as mp
+import queue
+import threading
+from concurrent.futures import ThreadPoolExecutor
+from typing import List, Optional
+
+from PIL import Image
+
+
+def _to_png(img: Image.Image) -> bytes:
+    buf = io.BytesIO()
+    img.save(buf, format="PNG")
+    return buf.getvalue()
+
+
+def _from_png(b: bytes) -> Image.Image:
+    return Image.open(io.BytesIO(b)).convert("RGB")
+
+
+def _worker_main(rank: int, device_index: Optional[int], loader_spec: str, do_warmup: bool,
+                 req_q, res_q):
+    """Worker process: pin the GPU, load the pipeline, serve jobs until a None arrives."""
+    try:
+        import torch
+        from .server import _import, process_image_sync, warmup
+        if device_index is not None and torch.cuda.is_available():
+            torch.cuda.set_device(device_index)
+        pipe = _import(loader_spec)()
+        if do_warmup:
+            warmup(pipe)
+        res_q.put(("ready", rank, None))
+    except Exception as e:  # report and exit: the dispatcher marks this worker dead
+        res_q.put(("dead", rank, f"{type(e).__name__}: {e}"))
+        return
+    while True:
+        job = req_q.get()
+        if job is None:
+            break
+        png, prompt, steps, use_cfg = job
+        try:
+            out = process_image_sync(pipe, _from_png(png), prompt, steps, use_cfg)
+            res_q.put(("ok", rank, _to_png(out)))
+        except Exception as e:
+            res_q.put(("err", rank, f"{e}"))
+
+
+class GpuDispatcher:
+    """``size`` worker processes (one per GPU, device ``devices[i]``), one request each.
+
+    Same worker protocol as ``server.LocalWorker``: ``try_acquire() -> token | None``,
+    ``run(token, image, request)`` (blocking, on ``executor``), ``release(token)``.
+    """
+
+    def __init__(self, size: int, loader_spec: str, devices: Optional[List[Optional[int]]] = None,
+                 do_warmup: bool = True, start_timeout: float = 1800.0):
+        self.size = size
+        self.loader_spec = loader_spec
+        self.devices = list(devices) if devices is not None else list(range(size))
+        self.do_warmup = do_warmup
+        self.start_timeout = start_timeout
+        self.executor = ThreadPoolExecutor(max_workers=size)
+        self._lock = threading.Lock()
+        self._free: List[int] = []
+        self._procs = []
+        self._req = []
+        self._res = []
+        self.errors = {}
+
+    @property
+    def loaded(self) -> bool:
+        return bool(self._procs) and len(self.errors) < self.size
+
+    def start(self):
+        import torch
+        if torch.cuda.is_initialized():
+            raise RuntimeError("GpuDispatcher.start() must run before this process touches the GPU")
+        ctx = mp.get_context("spawn")
+        for r in range(self.size):
+            rq, sq = ctx.Queue(), ctx.Queue()
+            p = ctx.Process(target=_worker_main, args=(r, self.devices[r], self.loader_spec,
+                                                       self.do_warmup, rq, sq), daemon=True)
+            p.start()
+            self._procs.append(p)
+            self._req.append(rq)
+            self._res.append(sq)
+        for r in range(self.size):
+            try:
+                kind, rank, msg = self._res[r].get(timeout=self.start_timeout)
+            except queue.Empty:
+                kind, rank, msg = "dead", r, "timed out while loading"
+            if kind == "ready":
+                self._free.append(rank)
+            else:
+                self.errors[rank] = msg
+
+    def try_acquire(self) -> Optional[int]:
+        with self._lock:
+            return self._free.pop(0) if self._free else None
+
+    def release(self, token: int):
+        with self._lock:
+            self._free.append(token)
+
+    def run(self, token: int, image: Image.Image, req) -> Image.Image:
+        self._req[token].put((_to_png(image), req.prompt, req.steps, req.use_cfg))
+        kind, _, payload = self._res[token].get()
+        if kind != "ok":
+            raise RuntimeError(payload)
+        return _from_png(payload)
+
+    def stop(self):
+        for q in self._req:
+            q.put(None)
+        for p in self._procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.terminate()
+        self._procs, self._free = [], []

@@ -74,8 +74,11 @@ class QwenImageEditPlusPipeline:
         names resolve only if a local snapshot directory of that name exists)."""
         if torch_dtype not in (BF16, None):
             raise ValueError("the HIP path computes in bf16 (the reference's torch_dtype)")
-        model = QwenImageTransformer2DModel(device=device, **config_overrides)
         path = pretrained_model_name_or_path
+        if path is not None and W.find_int8_files(path) and not W.find_transformer_files(path):
+            # pre-quantised image (weights.save_int8): int8 weights only, LoRA must be pre-fused
+            return cls(W.load_int8(path, device=device))
+        model = QwenImageTransformer2DModel(device=device, **config_overrides)
         if path is not None and W.find_transformer_files(path):
             W.load_transformer_weights(model, path)
         elif random_init_seed is not None or path is None:

@@ -67,19 +67,23 @@ class Transformer2DModelOutput:
 class _Block(nn.Module):
     """Packed weights of one QwenImageTransformerBlock."""
 
-    def __init__(self, D: int, Dh: int, F: int, device, dtype=BF16):
+    def __init__(self, D: int, Dh: int, F: int, device, dtype=BF16, int8_only: bool = False):
         super().__init__()
         e = dict(device=device, dtype=dtype)
+
+        def lin(*shape):  # bf16 weight of a quantised linear: absent when loaded pre-quantised
+            return torch.empty(0, **e) if int8_only else torch.empty(*shape, **e)
+
         for s in ("img", "txt"):
             self.register_buffer(f"w_mod_{s}", torch.empty(6 * D, D, **e))
             self.register_buffer(f"b_mod_{s}", torch.empty(6 * D, **e))
-            self.register_buffer(f"w_qkv_{s}", torch.empty(3 * D, D, **e))
+            self.register_buffer(f"w_qkv_{s}", lin(3 * D, D))
             self.register_buffer(f"b_qkv_{s}", torch.empty(3 * D, **e))
-            self.register_buffer(f"w_out_{s}", torch.empty(D, D, **e))
+            self.register_buffer(f"w_out_{s}", lin(D, D))
             self.register_buffer(f"b_out_{s}", torch.empty(D, **e))
-            self.register_buffer(f"w_up_{s}", torch.empty(F, D, **e))
+            self.register_buffer(f"w_up_{s}", lin(F, D))
             self.register_buffer(f"b_up_{s}", torch.empty(F, **e))
-            self.register_buffer(f"w_down_{s}", torch.empty(D, F, **e))
+            self.register_buffer(f"w_down_{s}", lin(D, F))
             self.register_buffer(f"b_down_{s}", torch.empty(D, **e))
         for n in ("norm_q", "norm_k", "norm_added_q", "norm_added_k"):
             self.register_buffer(n, torch.empty(Dh, **e))
@@ -127,7 +131,10 @@ class QwenImageTransformer2DModel(nn.Module):
     def __init__(self, patch_size: int = 2, in_channels: int = 64, out_channels: int = 16,
                  num_layers: int = 60, attention_head_dim: int = 128, num_attention_heads: int = 24,
                  joint_attention_dim: int = 3584, guidance_embeds: bool = False,
-                 axes_dims_rope: Tuple[int, int, int] = (16, 56, 56), device="cuda"):
+                 axes_dims_rope: Tuple[int, int, int] = (16, 56, 56), device="cuda",
+                 int8_only: bool = False):
+        """``int8_only``: allocate no bf16 copy of the eight quantised block linears; the
+        weights then come from a pre-quantised file (``weights.load_int8``)."""
         super().__init__()
         self.config = TransformerConfig(patch_size, in_channels, out_channels, num_layers,
                                         attention_head_dim, num_attention_heads, joint_attention_dim,
@@ -154,8 +161,10 @@ class QwenImageTransformer2DModel(nn.Module):
         self.register_buffer("norm_out_b", torch.empty(2 * D, **e))
         self.register_buffer("proj_out_w", torch.empty(P, D, **e))
         self.register_buffer("proj_out_b", torch.empty(P, **e))
-        self.transformer_blocks = nn.ModuleList(_Block(D, Dh, F, device) for _ in range(num_layers))
+        self.transformer_blocks = nn.ModuleList(_Block(D, Dh, F, device, int8_only=int8_only)
+                                                for _ in range(num_layers))
         self.int8 = False
+        self.int8_only = int8_only
         # optional kernel probe: {"attention": [...], "mlp_up": [...]} lists of
         # (start, end) torch.cuda.Event pairs recorded on the launch stream
         self.probe: Optional[Dict[str, list]] = None
@@ -280,6 +289,8 @@ class QwenImageTransformer2DModel(nn.Module):
         """Int8Linear replacement pass (README.md:136-138 'replace nn.Linear with
         Int8Linear in transformer'): per-output-channel int8 weights + fp32
         scales for every block linear, computed by the HIP quantiser."""
+        if self.int8_only:
+            raise RuntimeError("int8_only model: already quantised, the bf16 weights are absent")
         for blk in self.transformer_blocks:
             blk.q8 = {}
             for n in self._I8_LINEARS:
@@ -293,8 +304,64 @@ class QwenImageTransformer2DModel(nn.Module):
         return self
 
     def _requantize_if_needed(self):
+        if self.int8_only:
+            raise RuntimeError("this model was loaded pre-quantised (int8_only): its bf16 linear weights "
+                               "are absent, so they cannot be changed and re-quantised; fuse LoRA "
+                               "before weights.save_int8")
         if self.int8:
             self.quantize_int8()
+
+    def int8_state_dict(self) -> Dict[str, torch.Tensor]:
+        """On-disk int8 image: ``transformer_blocks.{i}.{linear}.q8`` (int8
+        [N, K]) and ``.scale`` (fp32 [N]) for the eight quantised linears, every other packed
+        buffer under its own name. Block linears are stored packed (q|k|v in one [3D, D])."""
+        if not self.int8:
+            raise RuntimeError("call quantize_int8() first")
+        out = {}
+        skip = {f"w_{n}" for n in self._I8_LINEARS}
+        for name, t in self.named_buffers():
+            if name.split(".")[-1] in skip:
+                continue
+            out[name] = t
+        for i, blk in enumerate(self.transformer_blocks):
+            for n, (q, sc) in blk.q8.items():
+                out[f"transformer_blocks.{i}.{n}.q8"] = q
+                out[f"transformer_blocks.{i}.{n}.scale"] = sc
+        return out
+
+    @torch.no_grad()
+    def load_int8_state_dict(self, sd: Dict[str, torch.Tensor]):
+        """Inverse of :meth:`int8_state_dict` (strict: every key, every shape)."""
+        bufs = dict(self.named_buffers())
+        skip = {f"w_{n}" for n in self._I8_LINEARS}
+        want = {n for n in bufs if n.split(".")[-1] not in skip}
+        for i in range(self.config.num_layers):
+            for n in self._I8_LINEARS:
+                want |= {f"transformer_blocks.{i}.{n}.q8", f"transformer_blocks.{i}.{n}.scale"}
+        if set(sd) != want:
+            missing, extra = sorted(want - set(sd)), sorted(set(sd) - want)
+            raise KeyError(f"int8 image mismatch: missing {missing[:4]} extra {extra[:4]}")
+        dev = self.device
+        for n in want:
+            if n.endswith(".q8") or n.endswith(".scale"):
+                continue
+            if tuple(bufs[n].shape) != tuple(sd[n].shape):
+                raise ValueError(f"{n}: shape {tuple(sd[n].shape)} != {tuple(bufs[n].shape)}")
+            bufs[n].copy_(sd[n].to(dev, BF16))
+        D, F = self.config.inner_dim, 4 * self.config.inner_dim
+        shapes = {"qkv": (3 * D, D), "out": (D, D), "up": (F, D), "down": (D, F)}
+        for i, blk in enumerate(self.transformer_blocks):
+            blk.q8 = {}
+            for n in self._I8_LINEARS:
+                q, sc = sd[f"transformer_blocks.{i}.{n}.q8"], sd[f"transformer_blocks.{i}.{n}.scale"]
+                if q.dtype != torch.int8 or sc.dtype != torch.float32 or tuple(q.shape) != shapes[n[:-4]] \
+                        or tuple(sc.shape) != (q.shape[0],):
+                    raise ValueError(f"block {i} {n}: bad int8 tensors {q.dtype}{tuple(q.shape)} "
+                                     f"{sc.dtype}{tuple(sc.shape)}")
+                blk.q8[n] = (q.to(dev).contiguous(), sc.to(dev).contiguous())
+        self.int8 = True
+        self._ws.clear()
+        return self
 
     # ------------------------------------------------------------------ forward
     def _workspace(self, B, S_img, S_txt) -> _Workspace:

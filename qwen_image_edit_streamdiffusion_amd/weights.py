@@ -114,3 +114,71 @@ def load_lora_file(path: str, weight_name: Optional[str] = None) -> Dict[str, to
             f"LoRA file {f} not found (hub names such as 'lightx2v/Qwen-Image-Lightning' need a "
             "local snapshot: there is no network access)")
     return dict(iter_safetensors([f]))
+
+
+# ---------------------------------------------------------------------------------------------
+# Pre-quantised int8 image (the reference quantises at start-up with
+# bitsandbytes, benchmark_int8.py:72-84, and has no on-disk int8 format). The image holds the
+# W8A8 weights this build computes with: int8 [N, K] + fp32 per-row scales for the eight block
+# linears (packed: q|k|v in one matrix), bf16 for everything else. Loading it allocates no bf16
+# copy of those linears, so the DiT needs ~21 GB of HBM instead of 41 + 20.
+INT8_FORMAT = "qie-int8-v1"
+
+
+def save_int8(model, directory: str, blocks_per_shard: int = 10) -> list:
+    """Write ``model.int8_state_dict()`` as safetensors shards under ``directory``; the config and
+    format tag ride in each shard's metadata. Returns the written file names."""
+    import json
+    from safetensors.torch import save_file
+    sd = model.int8_state_dict()
+    L = model.config.num_layers
+    n_shards = max(1, (L + blocks_per_shard - 1) // blocks_per_shard)
+    import dataclasses
+    cfg = json.dumps(dataclasses.asdict(model.config))
+    os.makedirs(directory, exist_ok=True)
+
+    def shard_of(name: str) -> int:
+        if name.startswith("transformer_blocks."):
+            return int(name.split(".")[1]) // blocks_per_shard
+        return 0
+
+    files = []
+    for k in range(n_shards):
+        part = {n: t.detach().contiguous().cpu() for n, t in sd.items() if shard_of(n) == k}
+        fn = os.path.join(directory, f"qie_int8-{k + 1:05d}-of-{n_shards:05d}.safetensors")
+        save_file(part, fn, metadata={"format": INT8_FORMAT, "config": cfg, "shard": str(k)})
+        files.append(fn)
+    return files
+
+
+def find_int8_files(path: str):
+    if os.path.isfile(path) and path.endswith(".safetensors"):
+        return [path]
+    for sub in ("transformer_int8", "."):
+        files = sorted(glob.glob(os.path.join(path, sub, "qie_int8-*.safetensors")))
+        if files:
+            return files
+    return []
+
+
+def load_int8(path: str, device="cuda"):
+    """Build a ``QwenImageTransformer2DModel`` from a pre-quantised image (no bf16 copy of the
+    quantised linears is allocated). Safe loader only (safetensors)."""
+    import json
+    from safetensors import safe_open
+    from .transformer import QwenImageTransformer2DModel
+    files = find_int8_files(path)
+    if not files:
+        raise FileNotFoundError(f"no qie_int8-*.safetensors under {path}")
+    with safe_open(files[0], framework="pt", device="cpu") as fh:
+        meta = fh.metadata() or {}
+    if meta.get("format") != INT8_FORMAT:
+        raise ValueError(f"{files[0]}: format {meta.get('format')!r}, expected {INT8_FORMAT!r}")
+    cfg = json.loads(meta["config"])
+    model = QwenImageTransformer2DModel(device=device, int8_only=True, **cfg)
+    sd = {}
+    for f in files:
+        with safe_open(f, framework="pt", device="cpu") as fh:
+            for k in fh.keys():
+                sd[k] = fh.get_tensor(k).to(device)
+    return model.load_int8_state_dict(sd)

@@ -165,3 +165,24 @@ def test_lora_fuse_matches_dense_delta(dev, tiny):
     w = m._param_slot("transformer_blocks.0.attn.to_k.weight").float().cpu()
     exp = (params["transformer_blocks.0.attn.to_k.weight"].float() + Bm @ A).to(BF16).float()
     assert torch.equal(w, exp)
+
+
+def test_int8_image_roundtrip_bitwise(dev, tiny, tmp_path):
+    """a pre-quantised on-disk image reloads into a model that allocates no
+    bf16 copy of the quantised linears and computes bitwise the same forward."""
+    cfg, params, _ = tiny
+    from qwen_image_edit_streamdiffusion_amd import weights as W
+    from qwen_image_edit_streamdiffusion_amd import QwenImageEditPlusPipeline
+    m8 = make_model(cfg, params, dev).quantize_int8()
+    W.save_int8(m8, str(tmp_path / "transformer_int8"), blocks_per_shard=1)
+    m8b = W.load_int8(str(tmp_path), device=dev)
+    assert m8b.int8 and m8b.int8_only
+    assert m8b.transformer_blocks[0].w_up_img.numel() == 0
+    shapes = [(1, 8, 8), (1, 8, 8)]
+    hs, enc = _inputs(2, shapes, 16, cfg.joint_attention_dim, seed=8)
+    t = R.model_timestep(torch.tensor([1000.0, 20.0]))
+    a = m8(hs.to(dev), enc.to(dev), None, t.to(dev), [shapes] * 2, [16, 16], return_dict=False)[0]
+    b = m8b(hs.to(dev), enc.to(dev), None, t.to(dev), [shapes] * 2, [16, 16], return_dict=False)[0]
+    assert torch.equal(a, b)
+    pipe = QwenImageEditPlusPipeline.from_pretrained(str(tmp_path), device=dev)
+    assert pipe.transformer.int8_only
