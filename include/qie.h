@@ -180,6 +180,44 @@ int qie_linear_qkv_i8(const void* xq, int64_t ldx, const float* sx, const void* 
                       int rows_per_batch, int seq_offset, int batch, int heads, int head_dim,
                       int s_pad, qie_stream_t stream);
 
+/* ---- split-K linears for short-M shapes (the text stream, M = B * S_txt) ---------------------
+ * Replaces the same diffusers linears as the entry points above (text-stream add_q/k/v_proj,
+ * to_add_out, txt_mlp: transformer_qwenimage.py [U]) for shapes whose
+ * output tiles cannot fill the chip (M = 432 gives 96 tiles for N = 3072). K is cut into
+ * `splits` equal ranges (K must be a multiple of splits * 64 bf16 / splits * 128 int8). Each
+ * range writes its partial sums to `workspace`, and a second kernel adds them in range order
+ * and applies the epilogue described by `epi`.
+ *   - workspace: caller-owned, >= splits * M * N * 4 bytes. Partials are fp32 for bf16 and
+ *     int32 for int8, so the int8 result is bitwise the unsplit one.
+ *   - The per-row arithmetic depends only on (K, splits), never on M, so rows stay batch
+ *     independent (batched CFG == sequential). */
+#define QIE_EPI_BIAS 0           /* y = bf16(x.W^T + b)                                        */
+#define QIE_EPI_GELU 1           /* y = gelu_tanh(bf16(x.W^T + b))                             */
+#define QIE_EPI_GATED_RESIDUAL 2 /* resid += bf16(gate[row/rows_per_batch] * bf16(x.W^T + b)) */
+#define QIE_EPI_QKV 3            /* scatter into qkv[3][batch][heads][s_pad][head_dim]         */
+
+typedef struct qie_epilogue {
+  int kind;              /* QIE_EPI_* */
+  void* out;             /* y (BIAS, GELU) / resid (GATED_RESIDUAL, in place) / qkv (QKV) */
+  int64_t ldo;           /* row stride of y / resid in elements (unused for QKV) */
+  const void* gate;      /* GATED_RESIDUAL: bf16 [batch][gate_bstride] */
+  int64_t gate_bstride;
+  int rows_per_batch;    /* GATED_RESIDUAL, QKV */
+  int seq_offset;        /* QKV, as qie_linear_qkv_bf16 */
+  int batch;
+  int heads;
+  int head_dim;
+  int s_pad;
+} qie_epilogue_t;
+
+int qie_linear_splitk_bf16(const void* x, int64_t ldx, const void* w, const void* bias,
+                           const qie_epilogue_t* epi, int M, int N, int K, int splits,
+                           void* workspace, int64_t workspace_bytes, qie_stream_t stream);
+int qie_linear_splitk_i8(const void* xq, int64_t ldx, const float* sx, const void* wq,
+                         const float* sw, const void* bias, const qie_epilogue_t* epi, int M,
+                         int N, int K, int splits, void* workspace, int64_t workspace_bytes,
+                         qie_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

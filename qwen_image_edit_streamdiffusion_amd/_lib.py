@@ -20,6 +20,17 @@ F = c_float
 FP = POINTER(c_float)
 IP = POINTER(c_int)
 
+
+
+class Epilogue(ctypes.Structure):
+    """``qie_epilogue_t`` (include/qie.h): epilogue of the split-K linears."""
+    _fields_ = [("kind", c_int), ("out", c_void_p), ("ldo", c_int64), ("gate", c_void_p),
+                ("gate_bstride", c_int64), ("rows_per_batch", c_int), ("seq_offset", c_int),
+                ("batch", c_int), ("heads", c_int), ("head_dim", c_int), ("s_pad", c_int)]
+
+
+EPI_BIAS, EPI_GELU, EPI_GATED_RESIDUAL, EPI_QKV = 0, 1, 2, 3
+
 # name -> argtypes (return type is always c_int unless listed in _RESTYPES)
 SIGNATURES = {
     "qie_abi_version": [],
@@ -44,6 +55,8 @@ SIGNATURES = {
     "qie_linear_i8": [P, L, P, P, P, P, P, L, I, I, I, I, P],
     "qie_linear_gated_residual_i8": [P, L, P, P, P, P, P, L, I, P, L, I, I, I, P],
     "qie_linear_qkv_i8": [P, L, P, P, P, P, P, I, I, I, I, I, I, I, I, P],
+    "qie_linear_splitk_bf16": [P, L, P, P, P, I, I, I, I, P, L, P],
+    "qie_linear_splitk_i8": [P, L, P, P, P, P, P, I, I, I, I, P, L, P],
 }
 _RESTYPES = {"qie_strerror": c_char_p}
 

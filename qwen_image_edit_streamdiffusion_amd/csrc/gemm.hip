@@ -27,7 +27,7 @@ namespace {
 
 constexpr int kRowBytes = 128;  // one LDS tile row = 64 bf16 or 128 int8 of K
 
-enum Epi { EPI_BIAS = 0, EPI_GELU = 1, EPI_GATE_RES = 2, EPI_QKV = 3 };
+enum Epi { EPI_BIAS = 0, EPI_GELU = 1, EPI_GATE_RES = 2, EPI_QKV = 3, EPI_PARTIAL = 4 };
 
 struct EpiArgs {
   void* out;          // y / resid / qkv base
@@ -41,6 +41,8 @@ struct EpiArgs {
   // int8 scales
   const float* sx;
   const float* sw;
+  // split-K partial sums (EPI_PARTIAL): [splits][M][N] fp32 (bf16) or int32 (int8)
+  void* ws;
 };
 
 __device__ __forceinline__ int swz_chunk(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
@@ -226,8 +228,10 @@ __global__ void __launch_bounds__(WM* WN * 64)
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int wm = wave / WN, wn = wave % WN;
 
-  const char* xg = X + (int64_t)m0 * ldx_b;
-  const char* wg = W + (int64_t)n0 * ldw_b;
+  // split-K: blockIdx.y selects a K range of K_bytes (gridDim.y == 1 otherwise)
+  const int64_t koff = (int64_t)blockIdx.y * K_bytes;
+  const char* xg = X + (int64_t)m0 * ldx_b + koff;
+  const char* wg = W + (int64_t)n0 * ldw_b + koff;
   const int m_valid = M - m0, n_valid = N - n0;
 
   typename Op::acc acc[MT][NTL];
@@ -288,10 +292,14 @@ __global__ void __launch_bounds__(WM* WN * 64)
     for (int j = 0; j < NTL; ++j) {
       const int n = n0 + wn * TN + j * 16 + (lane >> 4) * 4;
       if (n >= N) continue;
-      float v[4];
+      if constexpr (EPI == EPI_PARTIAL) {  // raw fp32 / int32 partial sums, 16 bytes per lane
+        *(typename Op::acc*)((char*)e.ws + (((int64_t)blockIdx.y * M + m) * N + n) * 4) = acc[i][j];
+      } else {
+        float v[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = acc_val<I8>(acc[i][j], r, 1.0f);
-      epilogue4<EPI, I8>(e, m, n, v);
+        for (int r = 0; r < 4; ++r) v[r] = acc_val<I8>(acc[i][j], r, 1.0f);
+        epilogue4<EPI, I8>(e, m, n, v);
+      }
     }
   }
 }
@@ -543,6 +551,58 @@ int launch_gemm(const void* x, int64_t ldx, const void* w, int64_t ldw, int M, i
   return qie_last_error();
 }
 
+// Split-K reduce: adds the `splits` partial sums of 4 consecutive columns in range order (fp32
+// for bf16, int32 for int8 -- the int8 total is then exactly the unsplit accumulator) and runs
+// the same epilogue as the unsplit kernels.
+template <int EPI, bool I8>
+__global__ void __launch_bounds__(256) splitk_reduce_kernel(EpiArgs e, int M, int N, int splits) {
+  const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int n4 = N >> 2;
+  if (q >= (int64_t)M * n4) return;
+  const int m = (int)(q / n4), n = (int)(q - (int64_t)m * n4) * 4;
+  const int64_t plane = (int64_t)M * N;
+  float v[4];
+  if constexpr (I8) {
+    const i32x4_t* p = (const i32x4_t*)e.ws + q;
+    i32x4_t t = p[0];
+    for (int s = 1; s < splits; ++s) t += *(const i32x4_t*)((const int*)p + s * plane);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = (float)t[r];
+  } else {
+    const f32x4_t* p = (const f32x4_t*)e.ws + q;
+    f32x4_t t = p[0];
+    for (int s = 1; s < splits; ++s) t += *(const f32x4_t*)((const float*)p + s * plane);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = t[r];
+  }
+  epilogue4<EPI, I8>(e, m, n, v);
+}
+
+template <bool I8>
+int launch_splitk(const void* x, int64_t ldx, const void* w, int M, int N, int K, int splits,
+                  int epi_kind, EpiArgs e, int64_t ws_bytes, hipStream_t s) {
+  const int eb = I8 ? 1 : 2;
+  QIE_CHECK_ARG(x && w && e.out && e.bias && e.ws);
+  QIE_CHECK_ARG(M > 0 && N > 0 && K > 0 && N % 4 == 0 && splits >= 1 && splits <= 64);
+  QIE_CHECK_ARG((K * eb) % (splits * kRowBytes) == 0);
+  QIE_CHECK_ARG(((ldx * eb) % 16) == 0 && ((uintptr_t)x % 16) == 0 && ((uintptr_t)w % 16) == 0);
+  QIE_CHECK_ARG(((uintptr_t)e.ws % 16) == 0 && ws_bytes >= (int64_t)splits * M * N * 4);
+  const int kb = K * eb / splits;
+  const dim3 grid(((M + 127) / 128) * ((N + 127) / 128), splits);
+  gemm_kernel<128, 128, 2, 2, EPI_PARTIAL, I8><<<grid, 256, 0, s>>>((const char*)x, ldx * eb,
+                                                                   (const char*)w, (int64_t)K * eb,
+                                                                   M, N, kb, e);
+  const int64_t nq = (int64_t)M * (N / 4);
+  const int nb = (int)((nq + 255) / 256);
+  switch (epi_kind) {
+    case EPI_BIAS: splitk_reduce_kernel<EPI_BIAS, I8><<<nb, 256, 0, s>>>(e, M, N, splits); break;
+    case EPI_GELU: splitk_reduce_kernel<EPI_GELU, I8><<<nb, 256, 0, s>>>(e, M, N, splits); break;
+    case EPI_GATE_RES: splitk_reduce_kernel<EPI_GATE_RES, I8><<<nb, 256, 0, s>>>(e, M, N, splits); break;
+    default: splitk_reduce_kernel<EPI_QKV, I8><<<nb, 256, 0, s>>>(e, M, N, splits); break;
+  }
+  return qie_last_error();
+}
+
 EpiArgs make_epi(void* out, int64_t ldo, const void* bias) {
   EpiArgs e{};
   e.out = out;
@@ -643,4 +703,53 @@ extern "C" int qie_linear_qkv_i8(const void* xq, int64_t ldx, const float* sx, c
   if (rc) return rc;
   return launch_gemm<EPI_QKV, true>(xq, ldx, wq, K, M, 3 * heads * head_dim, K, e,
                                     (hipStream_t)stream);
+}
+
+// ---------------------------------------------------------------------------- split-K C ABI
+static int splitk_epi(const qie_epilogue_t* p, const void* bias, int M, int N, void* ws, EpiArgs& e) {
+  QIE_CHECK_ARG(p && p->out);
+  e = make_epi(p->out, p->ldo, bias);
+  e.ws = ws;
+  switch (p->kind) {
+    case QIE_EPI_BIAS:
+    case QIE_EPI_GELU:
+      QIE_CHECK_ARG(p->ldo >= N && p->ldo % 4 == 0 && ((uintptr_t)p->out % 8) == 0);
+      return QIE_OK;
+    case QIE_EPI_GATED_RESIDUAL:
+      QIE_CHECK_ARG(p->gate && p->rows_per_batch > 0 && p->ldo >= N && p->ldo % 4 == 0 &&
+                    p->gate_bstride % 4 == 0);
+      e.gate = (const bf16_t*)p->gate;
+      e.gate_bstride = p->gate_bstride;
+      e.rows_per_batch = p->rows_per_batch;
+      return QIE_OK;
+    case QIE_EPI_QKV:
+      QIE_CHECK_ARG(N == 3 * p->heads * p->head_dim);
+      return qkv_args(e, M, p->rows_per_batch, p->seq_offset, p->batch, p->heads, p->head_dim, p->s_pad);
+    default:
+      return QIE_ERR_INVALID;
+  }
+}
+
+extern "C" int qie_linear_splitk_bf16(const void* x, int64_t ldx, const void* w, const void* bias,
+                                      const qie_epilogue_t* epi, int M, int N, int K, int splits,
+                                      void* workspace, int64_t workspace_bytes, qie_stream_t stream) {
+  EpiArgs e;
+  int rc = splitk_epi(epi, bias, M, N, workspace, e);
+  if (rc) return rc;
+  return launch_splitk<false>(x, ldx, w, M, N, K, splits, epi->kind, e, workspace_bytes,
+                              (hipStream_t)stream);
+}
+
+extern "C" int qie_linear_splitk_i8(const void* xq, int64_t ldx, const float* sx, const void* wq,
+                                    const float* sw, const void* bias, const qie_epilogue_t* epi,
+                                    int M, int N, int K, int splits, void* workspace,
+                                    int64_t workspace_bytes, qie_stream_t stream) {
+  QIE_CHECK_ARG(sx && sw);
+  EpiArgs e;
+  int rc = splitk_epi(epi, bias, M, N, workspace, e);
+  if (rc) return rc;
+  e.sx = sx;
+  e.sw = sw;
+  return launch_splitk<true>(xq, ldx, wq, M, N, K, splits, epi->kind, e, workspace_bytes,
+                             (hipStream_t)stream);
 }

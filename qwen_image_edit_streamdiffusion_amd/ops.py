@@ -293,3 +293,69 @@ def linear_qkv_i8(xq, sx, wq, sw, b, qkv, rows_per_batch: int, seq_offset: int):
     _chk(M == B * rows_per_batch and seq_offset + rows_per_batch <= S_pad, "i8 qkv rows")
     _lib.call("qie_linear_qkv_i8", _p(xq), xq.stride(0), _p(sx), _p(wq), _p(sw), _p(b), _p(qkv), M, K,
               rows_per_batch, seq_offset, B, H, Dh, S_pad, _stream())
+
+
+# ---------------------------------------------------------------------------- split-K linears
+EPI_BIAS, EPI_GELU, EPI_GATED_RESIDUAL, EPI_QKV = (_lib.EPI_BIAS, _lib.EPI_GELU, _lib.EPI_GATED_RESIDUAL,
+                                                    _lib.EPI_QKV)
+
+def splitk_splits(N: int, K: int, int8: bool = False) -> int:
+    """K-range count for the text-stream (short-M) linears. A function of (N, K) only -- never
+    of M -- so a row's arithmetic is the same at every batch size (batched CFG == sequential).
+    Aims at >= ~768 work-groups for M ~ 432 (4 row tiles) with >= 12 K-steps per range."""
+    steps = (K * (1 if int8 else 2)) // 128
+    want = max(1, -(-768 // (4 * max(1, -(-N // 128)))))
+    s = 1
+    while s < want and steps % (2 * s) == 0 and steps // (2 * s) >= 12:
+        s *= 2
+    return s
+
+
+def splitk_workspace_bytes(M: int, N: int, splits: int) -> int:
+    return splits * M * N * 4
+
+
+def _epilogue(kind: int, out: torch.Tensor, gate=None, rows_per_batch: int = 1, seq_offset: int = 0):
+    e = _lib.Epilogue()
+    e.kind = kind
+    e.out = _p(out)
+    if kind == _lib.EPI_QKV:
+        _chk(out.dim() == 5 and out.is_contiguous() and out.shape[0] == 3, "qkv [3,B,H,S_pad,Dh]")
+        _, e.batch, e.heads, e.s_pad, e.head_dim = out.shape
+        e.rows_per_batch, e.seq_offset = rows_per_batch, seq_offset
+        _chk(seq_offset + rows_per_batch <= e.s_pad, "qkv rows")
+    else:
+        _chk(out.dim() == 2 and out.stride(1) == 1 and out.dtype == BF16, "out [M, N] bf16")
+        e.ldo = out.stride(0)
+        if kind == _lib.EPI_GATED_RESIDUAL:
+            _chk(gate is not None and gate.dim() == 2 and gate.stride(1) == 1, "gate [B, >=N]")
+            e.gate, e.gate_bstride, e.rows_per_batch = _p(gate), gate.stride(0), rows_per_batch
+    return e
+
+
+def linear_splitk(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, kind: int, out: torch.Tensor,
+                  workspace: torch.Tensor, splits: int, gate=None, rows_per_batch: int = 1,
+                  seq_offset: int = 0):
+    """Split-K form of linear / linear_gated_residual / linear_qkv (``kind`` = _lib.EPI_*)."""
+    _dev(x, w, b, out, workspace)
+    M, K = x.shape
+    N = w.shape[0]
+    _chk(_is2d_rowmajor(x) and w.shape[1] == K and b.numel() == N, "split-K shapes")
+    _chk(workspace.numel() * workspace.element_size() >= splitk_workspace_bytes(M, N, splits), "workspace")
+    e = _epilogue(kind, out, gate, rows_per_batch, seq_offset)
+    _lib.call("qie_linear_splitk_bf16", _p(x), x.stride(0), _p(w), _p(b), ctypes.addressof(e), M, N, K,
+              splits, _p(workspace), workspace.numel() * workspace.element_size(), _stream())
+    return out
+
+
+def linear_splitk_i8(xq, sx, wq, sw, b, kind: int, out: torch.Tensor, workspace: torch.Tensor,
+                     splits: int, gate=None, rows_per_batch: int = 1, seq_offset: int = 0):
+    M, K = xq.shape
+    N = wq.shape[0]
+    _chk(xq.dtype == torch.int8 and wq.dtype == torch.int8 and wq.shape[1] == K, "i8 split-K")
+    _chk(workspace.numel() * workspace.element_size() >= splitk_workspace_bytes(M, N, splits), "workspace")
+    e = _epilogue(kind, out, gate, rows_per_batch, seq_offset)
+    _lib.call("qie_linear_splitk_i8", _p(xq), xq.stride(0), _p(sx), _p(wq), _p(sw), _p(b),
+              ctypes.addressof(e), M, N, K, splits, _p(workspace),
+              workspace.numel() * workspace.element_size(), _stream())
+    return out

@@ -106,6 +106,9 @@ class _Workspace:
         self.mlp_img = torch.empty(R_i, F, **e)
         self.mlp_txt = torch.empty(max(R_t, 1), F, **e)
         self.qkv = torch.zeros(3, B, H, self.S_pad, Dh, **e)  # pad rows stay 0 (finite V)
+        # split-K partial sums of the text-stream linears (fp32 / int32)
+        sk = max(ops.splitk_splits(n, k, int8) * n for n, k in ((3 * D, D), (D, D), (F, D), (D, F)))
+        self.splitk = torch.empty(max(R_t * sk, 4), device=device, dtype=torch.float32)
         self.txt_norm = torch.empty(max(R_t, 1), cfg.joint_attention_dim, **e)
         self.tproj = torch.empty(B, 256, **e)
         self.t_h = torch.empty(B, D, **e)
@@ -472,16 +475,15 @@ class QwenImageTransformer2DModel(nn.Module):
             streams.append(("txt", ws.x_txt[:R_t], ws.h_txt[:R_t], ws.att_txt[:R_t],
                             ws.mlp_txt[:R_t], mt, S_txt, S_img))
         # ---- LN1 + modulate, fused QKV projection into the joint buffer
+        QKV, GATE, GELU = ops.EPI_QKV, ops.EPI_GATED_RESIDUAL, ops.EPI_GELU
         for s, x, h, att, mlp, m, rpb, seq_off in streams:
             if i8:
                 qD, sc = self._q8(ws, s, x.shape[0], D)
                 ops.layernorm_modulate_i8(x, m[:, 0:D], m[:, D:2 * D], rpb, qD, sc, eps)
-                ops.linear_qkv_i8(qD, sc, *blk.q8[f"qkv_{s}"], getattr(blk, f"b_qkv_{s}"), ws.qkv, rpb,
-                                  seq_off)
+                self._linear(ws, blk, s, "qkv", (qD, sc), QKV, ws.qkv, rpb=rpb, seq_off=seq_off)
             else:
                 ops.layernorm_modulate(x, m[:, 0:D], m[:, D:2 * D], rpb, out=h, eps=eps)
-                ops.linear_qkv(h, getattr(blk, f"w_qkv_{s}"), getattr(blk, f"b_qkv_{s}"), ws.qkv, rpb,
-                               seq_off)
+                self._linear(ws, blk, s, "qkv", h, QKV, ws.qkv, rpb=rpb, seq_off=seq_off)
         # ---- QK RMSNorm + RoPE, joint attention
         ops.qk_norm_rope(ws.qkv, 0, S_img, blk.norm_q, blk.norm_k, icos, isin, eps)
         if has_txt:
@@ -494,25 +496,45 @@ class QwenImageTransformer2DModel(nn.Module):
                 rows, F = x.shape[0], mlp.shape[1]
                 qD, sc = self._q8(ws, s, rows, D)
                 ops.quantize_rows(att, qD, sc)
-                ops.linear_gated_residual_i8(qD, sc, *blk.q8[f"out_{s}"], getattr(blk, f"b_out_{s}"),
-                                             m[:, 2 * D:3 * D], rpb, x)
+                self._linear(ws, blk, s, "out", (qD, sc), GATE, x, gate=m[:, 2 * D:3 * D], rpb=rpb)
                 ops.layernorm_modulate_i8(x, m[:, 3 * D:4 * D], m[:, 4 * D:5 * D], rpb, qD, sc, eps)
                 with self._probe("mlp_up" if s == "img" else None):
-                    ops.linear_i8(qD, sc, *blk.q8[f"up_{s}"], getattr(blk, f"b_up_{s}"), mlp,
-                                  act=ops.ACT_GELU)
+                    self._linear(ws, blk, s, "up", (qD, sc), GELU, mlp)
                 qF, sc = self._q8(ws, s, rows, F)
                 ops.quantize_rows(mlp, qF, sc)
-                ops.linear_gated_residual_i8(qF, sc, *blk.q8[f"down_{s}"], getattr(blk, f"b_down_{s}"),
-                                             m[:, 5 * D:6 * D], rpb, x)
+                self._linear(ws, blk, s, "down", (qF, sc), GATE, x, gate=m[:, 5 * D:6 * D], rpb=rpb)
             else:
-                ops.linear_gated_residual(att, getattr(blk, f"w_out_{s}"), getattr(blk, f"b_out_{s}"),
-                                          m[:, 2 * D:3 * D], rpb, x)
+                self._linear(ws, blk, s, "out", att, GATE, x, gate=m[:, 2 * D:3 * D], rpb=rpb)
                 ops.layernorm_modulate(x, m[:, 3 * D:4 * D], m[:, 4 * D:5 * D], rpb, out=h, eps=eps)
                 with self._probe("mlp_up" if s == "img" else None):
-                    ops.linear(h, getattr(blk, f"w_up_{s}"), getattr(blk, f"b_up_{s}"), out=mlp,
-                               act=ops.ACT_GELU)
-                ops.linear_gated_residual(mlp, getattr(blk, f"w_down_{s}"), getattr(blk, f"b_down_{s}"),
-                                          m[:, 5 * D:6 * D], rpb, x)
+                    self._linear(ws, blk, s, "up", h, GELU, mlp)
+                self._linear(ws, blk, s, "down", mlp, GATE, x, gate=m[:, 5 * D:6 * D], rpb=rpb)
+
+    def _linear(self, ws, blk, s: str, name: str, inp, kind: int, out, gate=None, rpb: int = 1,
+                seq_off: int = 0):
+        """One block linear (+ fused epilogue). ``inp`` is a bf16 activation or an int8 (q, scale)
+        pair. Image stream: one launch of the ring / 2-stage kernel. Text stream (M = B * S_txt,
+        too few tiles to fill the chip): split-K into ``ws.splitk`` with a K-only split rule."""
+        b = getattr(blk, f"b_{name}_{s}")
+        if isinstance(inp, tuple):
+            (xq, sx), (wq, sw) = inp, blk.q8[f"{name}_{s}"]
+            if s == "txt":
+                sp = ops.splitk_splits(wq.shape[0], wq.shape[1], int8=True)
+                return ops.linear_splitk_i8(xq, sx, wq, sw, b, kind, out, ws.splitk, sp, gate, rpb, seq_off)
+            if kind == ops.EPI_QKV:
+                return ops.linear_qkv_i8(xq, sx, wq, sw, b, out, rpb, seq_off)
+            if kind == ops.EPI_GATED_RESIDUAL:
+                return ops.linear_gated_residual_i8(xq, sx, wq, sw, b, gate, rpb, out)
+            return ops.linear_i8(xq, sx, wq, sw, b, out, act=ops.ACT_GELU if kind == ops.EPI_GELU else ops.ACT_NONE)
+        w = getattr(blk, f"w_{name}_{s}")
+        if s == "txt":
+            sp = ops.splitk_splits(w.shape[0], w.shape[1])
+            return ops.linear_splitk(inp, w, b, kind, out, ws.splitk, sp, gate, rpb, seq_off)
+        if kind == ops.EPI_QKV:
+            return ops.linear_qkv(inp, w, b, out, rpb, seq_off)
+        if kind == ops.EPI_GATED_RESIDUAL:
+            return ops.linear_gated_residual(inp, w, b, gate, rpb, out)
+        return ops.linear(inp, w, b, out=out, act=ops.ACT_GELU if kind == ops.EPI_GELU else ops.ACT_NONE)
 
     @contextlib.contextmanager
     def _probe(self, name: Optional[str]):

@@ -68,3 +68,12 @@ def test_invalid_arguments_rejected_on_host(lib):
     assert lib.qie_qk_norm_rope_bf16(16, 1, 1, 64, 256, 0, 8, 16, 16, 16, 16, 1e-6, None) == -1
     with pytest.raises(_lib.QieError):
         _lib.call("qie_rmsnorm_bf16", None, None, None, 1, 8, 1e-6, None)
+    # split-K: null epilogue, unknown kind, K not a multiple of splits * 64, workspace too small
+    e = _lib.Epilogue(kind=0, out=16, ldo=256)
+    ep = ctypes.addressof(e)
+    assert lib.qie_linear_splitk_bf16(16, 256, 16, 16, None, 8, 256, 256, 2, 16, 1 << 20, None) == -1
+    bad = _lib.Epilogue(kind=9, out=16, ldo=256)
+    assert lib.qie_linear_splitk_bf16(16, 256, 16, 16, ctypes.addressof(bad), 8, 256, 256, 2, 16, 1 << 20, None) == -1
+    assert lib.qie_linear_splitk_bf16(16, 256, 16, 16, ep, 8, 256, 192, 2, 16, 1 << 20, None) == -1
+    assert lib.qie_linear_splitk_bf16(16, 256, 16, 16, ep, 8, 256, 256, 2, 16, 8 * 256 * 4, None) == -1
+    assert lib.qie_linear_splitk_i8(16, 256, None, 16, 16, 16, ep, 8, 256, 256, 2, 16, 1 << 20, None) == -1

@@ -296,3 +296,72 @@ def test_linear_i8_gated_and_qkv(dev):
     ops.linear_gated_residual_i8(xq, sx, wq[:N], sw[:N], b[:N], gate, rpb, resid)
     exp = R.gated_residual(r0.view(B, rpb, N), gate.cpu(), ref[:, :N].reshape(B, rpb, N), RB)
     close(resid, exp.view(B * rpb, N))
+
+
+# ------------------------------------------------------------------ split-K (text-stream) linears
+@pytest.mark.parametrize("M,N,K,splits", [(432, 3072, 3072, 4), (216, 3072, 12288, 8), (37, 512, 1024, 2),
+                                          (432, 1024, 768, 3), (130, 256, 512, 1)])
+@pytest.mark.parametrize("kind", [0, 1, 2])
+def test_linear_splitk_vs_oracle(dev, M, N, K, splits, kind):
+    """bf16 split-K: same tolerances as the unsplit GEMM (only the fp32 sum order differs)."""
+    ops = _ops()
+    x, w, b = rnd((M, K), dev, 1.0, 60), rnd((N, K), dev, 0.05, 61), rnd((N,), dev, 0.1, 62)
+    ws = torch.empty(ops.splitk_workspace_bytes(M, N, splits) // 4, device=dev)
+    lin = R.linear(x.cpu(), w.cpu(), b.cpu(), RB)
+    if kind == ops.EPI_GATED_RESIDUAL:
+        B = 2 if M % 2 == 0 else 1
+        rpb = M // B
+        gate = rnd((B, N), dev, 0.5, 63)
+        resid = rnd((M, N), dev, 1.0, 64)
+        ref = R.gated_residual(resid.cpu().float().view(B, rpb, N), gate.cpu(), lin.view(B, rpb, N), RB).view(M, N)
+        ops.linear_splitk(x, w, b, kind, resid, ws, splits, gate=gate, rows_per_batch=rpb)
+        close(resid, ref)
+    else:
+        y = torch.empty(M, N, dtype=BF16, device=dev)
+        ops.linear_splitk(x, w, b, kind, y, ws, splits)
+        close(y, R.gelu_tanh(lin, RB) if kind == ops.EPI_GELU else lin)
+
+
+def test_linear_splitk_qkv_matches_unsplit(dev):
+    ops = _ops()
+    B, H, Dh, rpb, s_pad, off, K = 2, 2, 128, 216, 512, 256, 3072
+    x, w, b = rnd((B * rpb, K), dev, 1.0, 65), rnd((3 * H * Dh, K), dev, 0.02, 66), rnd((3 * H * Dh,), dev, 0.1, 67)
+    a = torch.zeros(3, B, H, s_pad, Dh, dtype=BF16, device=dev)
+    c = torch.zeros_like(a)
+    ops.linear_qkv(x, w, b, a, rpb, off)
+    ws = torch.empty(ops.splitk_workspace_bytes(B * rpb, 3 * H * Dh, 4) // 4, device=dev)
+    ops.linear_splitk(x, w, b, ops.EPI_QKV, c, ws, 4, rows_per_batch=rpb, seq_offset=off)
+    close(c[:, :, :, off:off + rpb], a[:, :, :, off:off + rpb])
+    assert (c[:, :, :, :off] == 0).all() and (c[:, :, :, off + rpb:] == 0).all()
+
+
+@pytest.mark.parametrize("kind", [0, 1, 2, 3])
+def test_linear_splitk_i8_bitwise_equals_unsplit(dev, kind):
+    """int8 split-K sums int32 partials: bitwise the unsplit int8 result for every epilogue."""
+    ops = _ops()
+    g = torch.Generator().manual_seed(68)
+    B, rpb, K, H = 2, 216, 3072, 2
+    M, N = B * rpb, 3 * H * 128
+    xq = torch.randint(-127, 128, (M, K), generator=g, dtype=torch.int8).to(dev)
+    wq = torch.randint(-127, 128, (N, K), generator=g, dtype=torch.int8).to(dev)
+    sx = (torch.rand(M, generator=g) * 0.01 + 1e-3).to(dev)
+    sw = (torch.rand(N, generator=g) * 1e-3 + 1e-4).to(dev)
+    b = (torch.randn(N, generator=g) * 0.1).to(BF16).to(dev)
+    ws = torch.empty(ops.splitk_workspace_bytes(M, N, 4) // 4, device=dev)
+    if kind == ops.EPI_QKV:
+        a = torch.zeros(3, B, H, 512, 128, dtype=BF16, device=dev)
+        c = torch.zeros_like(a)
+        ops.linear_qkv_i8(xq, sx, wq, sw, b, a, rpb, 0)
+        ops.linear_splitk_i8(xq, sx, wq, sw, b, kind, c, ws, 4, rows_per_batch=rpb)
+    elif kind == ops.EPI_GATED_RESIDUAL:
+        gate = rnd((B, N), dev, 0.5, 69)
+        a = rnd((M, N), dev, 1.0, 70)
+        c = a.clone()
+        ops.linear_gated_residual_i8(xq, sx, wq, sw, b, gate, rpb, a)
+        ops.linear_splitk_i8(xq, sx, wq, sw, b, kind, c, ws, 4, gate=gate, rows_per_batch=rpb)
+    else:
+        a = torch.empty(M, N, dtype=BF16, device=dev)
+        c = torch.empty_like(a)
+        ops.linear_i8(xq, sx, wq, sw, b, a, act=kind)
+        ops.linear_splitk_i8(xq, sx, wq, sw, b, kind, c, ws, 4)
+    assert torch.equal(a, c)
