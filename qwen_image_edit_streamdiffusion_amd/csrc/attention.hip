@@ -22,6 +22,8 @@
 // K/V tiles are double buffered in LDS and register-staged: the next tile's
 // global loads are issued before the MFMAs and written after them (T14).
 // Workgroups of one (b, h) are placed on one XCD so its K/V stream from L2.
+#include <type_traits>
+
 #include "qie_common.h"
 
 namespace {
@@ -226,6 +228,328 @@ __global__ void __launch_bounds__(512) attn_fwd_kernel(AttnArgs a) {
   }
 }
 
+// =============================================================================================
+// Ping-pong variant (attn_pp_kernel). Same math, lane layout and LDS swizzles as
+// attn_fwd_kernel; only the schedule differs. Waves 0-3 (group 0) and 4-7 (group 1) put one
+// wave of each group on every SIMD. Group 1 runs one phase behind group 0, so while one wave
+// of a SIMD is in its MFMA phase the other is in its VALU phase:
+//   M-phase t : S(t) = K(t) Q^T (16 MFMA) then O += V(t-1)^T P(t-1)^T (16 MFMA), operands
+//               streamed from LDS three MFMAs ahead;
+//   V-phase t : masking, online softmax of S(t) -> P(t) (bf16), lazy O rescale, and the
+//               LDS-DMA of K(t+2) / V(t+1).
+// The MFMAs are asm volatile (their order and the LDS reads between them stay as written) and
+// empty register fences on S / O / P pin every softmax instruction inside its V-phase (hipcc
+// would otherwise hoist it between MFMAs, where the unpadded MFMA -> VALU hazard bites). K and
+// V live in 3-slot LDS rings filled by buffer_load...lds two tiles ahead. Waits: vmcnt(0) at
+// the end of an M-phase (this wave's pieces from its previous V-phase), vmcnt(pieces) at the
+// end of a V-phase; one barrier per phase.
+constexpr int kRing = 3;
+
+#ifdef QIE_ATTN_STAMP
+// diagnostic build only (tools/attn_stamp.hip): per-group sums of phase cycles
+__device__ unsigned long long g_stamp[2][6];
+#define STAMP(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#define STAMP_ADD(i, d) acc_st[i] += (d)
+#else
+#define STAMP(v)
+#define STAMP_ADD(i, d)
+#endif
+
+// Raw buffer descriptor (base, stride 0, num_records, dword3 0x00020000) in SGPRs.
+__device__ __forceinline__ i32x4_t attn_rsrc(const bf16_t* base, int bytes) {
+  const uint64_t p = (uint64_t)base;
+  return i32x4_t{__builtin_amdgcn_readfirstlane((int)(uint32_t)p),
+                 __builtin_amdgcn_readfirstlane((int)(uint32_t)(p >> 32)),
+                 __builtin_amdgcn_readfirstlane(bytes), 0x00020000};
+}
+// One 1-KiB LDS-DMA piece (buffer_load_dwordx4 ... lds) as inline asm: hipcc does not track it,
+// so it inserts no conservative vmcnt(0) before LDS reads it cannot prove disjoint from the
+// DMA target (the loop's own counted waits cover it). M0 is set and restored inside the
+// statement; s_nop 4 covers a just-readfirstlane'd SGPR operand (cdna_hip_programming §5.7).
+__device__ __forceinline__ void attn_dma(const i32x4_t& r, const char QIE_LDS* dst, uint32_t voff, int soff) {
+  unsigned keep;
+  const int lds = __builtin_amdgcn_readfirstlane((int)(uint32_t)(uintptr_t)dst);
+  asm volatile(
+      "s_nop 4\n\t"
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %3\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %2, %4 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(r), "s"(lds), "s"(soff)
+      : "memory");
+}
+__device__ __forceinline__ void mma32(f32x16_t& c, const bf16x8_t& a, const bf16x8_t& b) {
+  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(c) : "v"(a), "v"(b));
+}
+__device__ __forceinline__ void mma32_z(f32x16_t& c, const bf16x8_t& a, const bf16x8_t& b) {
+  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(c) : "v"(a), "v"(b));
+}
+template <typename T>
+__device__ __forceinline__ void rfence(T& x) {
+  asm volatile("" : "+v"(x));
+}
+
+struct PPState {
+  f32x16_t s[2];
+  f32x16_t o[4];
+  bf16x8_t pf[4];
+  bf16x8_t qf[8];
+  float m_run, l_run;
+};
+
+__global__ void __launch_bounds__(512) attn_pp_kernel(AttnArgs a) {
+  __shared__ __attribute__((aligned(16))) char smem_raw[2 * kRing * kTileBytes];  // K ring, V ring
+  char QIE_LDS* smem = (char QIE_LDS*)smem_raw;
+
+  const int nwg = a.qblocks * a.H * a.B;
+  const int wgid = xcd_remap(blockIdx.x, nwg);
+  const int qb = wgid % a.qblocks;
+  const int bh = wgid / a.qblocks;
+  const int h = bh % a.H, b = bh / a.H;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int grp = wave >> 2;
+  const int hf = lane >> 5;
+  const int ql = lane & 31;
+  const int64_t plane = (int64_t)a.s_pad * kDh;
+  const bf16_t* Qp = a.qkv + ((int64_t)(0 * a.B + b) * a.H + h) * plane;
+  const bf16_t* Kp = a.qkv + ((int64_t)(1 * a.B + b) * a.H + h) * plane;
+  const bf16_t* Vp = a.qkv + ((int64_t)(2 * a.B + b) * a.H + h) * plane;
+  const int kv_len = a.kv_len.v[b];
+  const int ntiles = (kv_len + kKB - 1) / kKB;
+
+  PPState st;
+#ifdef QIE_ATTN_STAMP
+  unsigned long long acc_st[6] = {0, 0, 0, 0, 0, 0};
+#endif
+  const int q_row = qb * kQB + wave * 32 + ql;
+  {
+    const bf16_t* qr = Qp + (int64_t)q_row * kDh + 8 * hf;
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) st.qf[ks] = *(const bf16x8_t*)(qr + 16 * ks);
+  }
+
+  // ---- LDS-DMA: wave w fills rows 4(w + 8p) .. +3 of a tile (p = 0, 1) for K and for V; the
+  // per-lane source chunk carries the XOR swizzle (LDS-DMA writes are lane-linear)
+  const auto kr = attn_rsrc(Kp, a.s_pad * kDh * 2);
+  const auto vr = attn_rsrc(Vp, a.s_pad * kDh * 2);
+  uint32_t ko[2], vo[2];
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const int row = (wave + 8 * p) * 4 + (lane >> 4), c = lane & 15;
+    ko[p] = row * 256 + ((c ^ (row & 15)) << 4);
+    vo[p] = row * 256 + ((c ^ ((row & 3) << 2)) << 4);
+  }
+  auto dmaK = [&](int t) {
+    char QIE_LDS* base = smem + (t % kRing) * kTileBytes;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) attn_dma(kr, base + (wave + 8 * p) * 1024, ko[p], t * kTileBytes);
+  };
+  auto dmaV = [&](int t) {
+    char QIE_LDS* base = smem + (kRing + t % kRing) * kTileBytes;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) attn_dma(vr, base + (wave + 8 * p) * 1024, vo[p], t * kTileBytes);
+  };
+
+  // per-lane LDS read offsets (as attn_fwd_kernel)
+  const int ksw = lane & 15;
+  const int tri = lane & 15;
+  const int tr_row = tri >> 2;
+  const int tr_sw = tr_row << 2;
+  const int tr_g1 = (lane >> 4) & 1;
+  const int tr_cb = 8 * (tri & 1);
+
+  // A operand of MFMA i of an M-phase: i < 16 -> K fragment (cb = i>>3, ks = i&7) of tile tk;
+  // i >= 16 -> V^T fragment (ks = (i-16)>>2, db = (i-16)&3) of tile tv
+  auto opA = [&](int i, int tk, int tv) -> bf16x8_t {
+    if (i < 16) {
+      const int cb = i >> 3, ks = i & 7;
+      const char QIE_LDS* krow = smem + (tk % kRing) * kTileBytes + (cb * 32 + ql) * 256;
+      return *(const bf16x8_t QIE_LDS*)(krow + (((2 * ks + hf) ^ ksw) << 4));
+    }
+    const int j = i - 16, ks = j >> 2, db = j & 3;
+    const char QIE_LDS* vb = smem + (kRing + tv % kRing) * kTileBytes;
+    const int r0 = 16 * ks + 4 * hf + tr_row;
+    const int chunk = (4 * db + 2 * tr_g1 + ((tri & 3) >> 1)) ^ tr_sw;
+    const char QIE_LDS* p0 = vb + r0 * 256 + (chunk << 4) + tr_cb;
+    const s16x4_t va = __builtin_amdgcn_ds_read_tr16_b64_v4i16((s16x4_t QIE_LDS*)p0);
+    const s16x4_t vb2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((s16x4_t QIE_LDS*)(p0 + 8 * 256));
+    typedef __attribute__((ext_vector_type(8))) short s16x8_t;
+    return __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(va, vb2, 0, 1, 2, 3, 4, 5, 6, 7));
+  };
+  auto mfma_i = [&](int i, const bf16x8_t& A) {
+    if (i < 16) {
+      const int cb = i >> 3, ks = i & 7;
+      if (ks == 0) mma32_z(st.s[cb], A, st.qf[0]);
+      else mma32(st.s[cb], A, st.qf[ks]);
+    } else {
+      const int j = i - 16;
+      mma32(st.o[j & 3], A, st.pf[j >> 2]);
+    }
+  };
+  // M-phase over MFMAs [i0, i1): operands prefetched three MFMAs ahead
+  auto mphase = [&](auto i0_t, auto i1_t, int tk, int tv, int td) {
+    constexpr int i0 = decltype(i0_t)::value, i1 = decltype(i1_t)::value;
+    const bool dk = td >= 0 && td + 2 < ntiles, dv = td >= 0 && td + 1 < ntiles;
+    bf16x8_t A[4];
+    // the MFMA wave outranks its SIMD partner (in its softmax phase) for issue: otherwise the
+    // older wave group wins arbitration and starves the younger group's MFMA phase
+    __builtin_amdgcn_s_setprio(2);
+#pragma unroll
+    for (int i = i0; i < i0 + 3 && i < i1; ++i) A[i & 3] = opA(i, tk, tv);
+#pragma unroll
+    for (int i = i0; i < i1; ++i) {
+      if (i + 3 < i1) A[(i + 3) & 3] = opA(i + 3, tk, tv);
+      mfma_i(i, A[i & 3]);
+#ifdef QIE_ATTN_DMA_M
+      // this phase's LDS-DMA pieces, one after every 8th MFMA: K(td+2) rows, then V(td+1)
+      if (i - i0 == 4 && dk) attn_dma(kr, smem + ((td + 2) % kRing) * kTileBytes + wave * 1024, ko[0], (td + 2) * kTileBytes);
+      if (i - i0 == 12 && dk) attn_dma(kr, smem + ((td + 2) % kRing) * kTileBytes + (wave + 8) * 1024, ko[1], (td + 2) * kTileBytes);
+      if (i - i0 == 20 && dv) attn_dma(vr, smem + (kRing + (td + 1) % kRing) * kTileBytes + wave * 1024, vo[0], (td + 1) * kTileBytes);
+      if (i - i0 == 28 && dv) attn_dma(vr, smem + (kRing + (td + 1) % kRing) * kTileBytes + (wave + 8) * 1024, vo[1], (td + 1) * kTileBytes);
+#endif
+    }
+    __builtin_amdgcn_s_setprio(0);
+  };
+  // V-phase: softmax of S(t) into P(t), DMA of later tiles; ends with the phase barrier
+  auto vphase = [&](int t) {
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb) rfence(st.s[cb]);
+#pragma unroll
+    for (int db = 0; db < 4; ++db) rfence(st.o[db]);
+    int pieces = 0;
+#ifndef QIE_ATTN_DMA_M
+    if (t + 2 < ntiles) { dmaK(t + 2); pieces += 2; }
+    if (t + 1 < ntiles) { dmaV(t + 1); pieces += 2; }
+#endif
+    const int kv0 = t * kKB;
+    if (kv0 + kKB > kv_len) {
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int kv = kv0 + cb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hf;
+          if (kv >= kv_len) st.s[cb][r] = -INFINITY;
+        }
+    }
+    const float c = a.c;
+    float m0 = fmaxf(st.s[0][0], st.s[0][1]), m1 = fmaxf(st.s[0][2], st.s[0][3]);
+#pragma unroll
+    for (int r = 4; r < 16; r += 2) { m0 = fmaxf(m0, st.s[0][r]); m1 = fmaxf(m1, st.s[0][r + 1]); }
+#pragma unroll
+    for (int r = 0; r < 16; r += 2) { m0 = fmaxf(m0, st.s[1][r]); m1 = fmaxf(m1, st.s[1][r + 1]); }
+    float mx = fmaxf(m0, m1);
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    if (__any((mx - st.m_run) * c > kRescaleThr)) {
+      const float m_new = fmaxf(st.m_run, mx);
+      const float alpha = __builtin_amdgcn_exp2f((st.m_run - m_new) * c);
+      st.m_run = m_new;
+      st.l_run *= alpha;
+#pragma unroll
+      for (int db = 0; db < 4; ++db) st.o[db] *= alpha;
+    }
+    const float mc = st.m_run * c;
+    float ps0 = 0.f, ps1 = 0.f;
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+      for (int r = 0; r < 16; r += 2) {
+        const float p0 = __builtin_amdgcn_exp2f(__builtin_fmaf(st.s[cb][r], c, -mc));
+        const float p1 = __builtin_amdgcn_exp2f(__builtin_fmaf(st.s[cb][r + 1], c, -mc));
+        ps0 += p0;
+        ps1 += p1;
+        st.pf[cb * 2 + (r >> 3)][r & 7] = (__bf16)p0;
+        st.pf[cb * 2 + (r >> 3)][(r & 7) + 1] = (__bf16)p1;
+      }
+    st.l_run += ps0 + ps1;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) rfence(st.pf[k]);
+    rfence(st.l_run);  // keep the row-sum adds in this phase (hipcc sinks them into the M-phase)
+    rfence(st.m_run);
+#pragma unroll
+    for (int db = 0; db < 4; ++db) rfence(st.o[db]);
+    if (pieces == 4) asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
+    else if (pieces == 2) asm volatile("s_waitcnt vmcnt(2)\n\ts_barrier" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I16 = std::integral_constant<int, 16>;
+  using I32 = std::integral_constant<int, 32>;
+
+  // ---- prologue: K(0), K(1), V(0) resident; group 1 waits one phase
+  dmaK(0);
+  if (ntiles > 1) dmaK(1);
+  dmaV(0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the asm DMA pieces
+  __builtin_amdgcn_s_waitcnt(0);                     // Q fragments (hipcc-tracked)
+  asm volatile("s_barrier" ::: "memory");
+  if (grp == 1) asm volatile("s_barrier" ::: "memory");
+#pragma unroll
+  for (int db = 0; db < 4; ++db) st.o[db] = f32x16_t{};
+  st.m_run = -INFINITY;
+  st.l_run = 0.f;
+
+#ifdef QIE_ATTN_DMA_M
+  // pieces issued in M-phase t stay in flight across its barrier; V-phase t ends with vmcnt(0)
+  auto mend = [&](int t) {
+    const int n = (t + 2 < ntiles ? 2 : 0) + (t + 1 < ntiles ? 2 : 0);
+    if (n == 4) asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
+    else if (n == 2) asm volatile("s_waitcnt vmcnt(2)\n\ts_barrier" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+  };
+#else
+  auto mend = [&](int) { asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory"); };
+#endif
+  mphase(I0{}, I16{}, 0, 0, 0);  // S(0)  (DMA of K(2), V(1) when issued in M-phases)
+  mend(0);
+  vphase(0);
+  for (int t = 1; t < ntiles; ++t) {
+    STAMP(t0);
+    mphase(I0{}, I32{}, t, t - 1, t);  // S(t), O += V(t-1) P(t-1)
+    STAMP(t1);
+    mend(t);
+    STAMP(t2);
+    vphase(t);
+    STAMP(t3);
+    STAMP_ADD(0, t1 - t0);  // M-phase body
+    STAMP_ADD(1, t2 - t1);  // M-end wait + barrier
+    STAMP_ADD(2, t3 - t2);  // V-phase body incl. its end barrier
+    STAMP_ADD(3, 1);
+  }
+#ifdef QIE_ATTN_STAMP
+  if (lane == 0)
+    for (int i = 0; i < 4; ++i) atomicAdd(&g_stamp[grp][i], acc_st[i]);
+#endif
+  mphase(I16{}, I32{}, 0, ntiles - 1, -1);  // O += V(T-1) P(T-1)
+  if (grp == 0) asm volatile("s_barrier" ::: "memory");
+  // MFMA D -> VALU read hazard before the epilogue reads O (asm MFMAs are not padded by hipcc)
+  asm volatile("s_nop 15\n\ts_nop 7" : "+v"(st.o[0]), "+v"(st.o[1]), "+v"(st.o[2]), "+v"(st.o[3]));
+
+  const float l_tot = st.l_run + __shfl_xor(st.l_run, 32, 64);
+  const float inv = 1.0f / l_tot;
+  const int s = q_row;
+  bf16_t* dst = nullptr;
+  if (s < a.s_img) {
+    dst = a.out_img + ((int64_t)b * a.s_img + s) * (a.H * kDh) + h * kDh;
+  } else if (s < a.s_img + a.txt_rows) {
+    dst = a.out_txt + ((int64_t)b * a.txt_rows + (s - a.s_img)) * (a.H * kDh) + h * kDh;
+  }
+  if (dst) {
+#pragma unroll
+    for (int db = 0; db < 4; ++db)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int d = 32 * db + 8 * g + 4 * hf;
+        const u32x2_t w = {pack2(st.o[db][4 * g] * inv, st.o[db][4 * g + 1] * inv),
+                           pack2(st.o[db][4 * g + 2] * inv, st.o[db][4 * g + 3] * inv)};
+        *(u32x2_t*)(dst + d) = w;
+      }
+  }
+}
+
 }  // namespace
 
 extern "C" int qie_attention_fwd_bf16(const void* qkv, int batch, int heads, int s_pad,
@@ -251,6 +575,10 @@ extern "C" int qie_attention_fwd_bf16(const void* qkv, int batch, int heads, int
     a.kv_len.v[i] = kv_len_host[i];
   }
   const int nwg = a.qblocks * heads * batch;
+#ifdef QIE_ATTN_PP
+  attn_pp_kernel<<<nwg, 512, 0, (hipStream_t)stream>>>(a);
+#else
   attn_fwd_kernel<<<nwg, 512, 0, (hipStream_t)stream>>>(a);
+#endif
   return qie_last_error();
 }
