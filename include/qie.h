@@ -116,6 +116,22 @@ int qie_attention_fwd_bf16(const void* qkv, int batch, int heads, int s_pad,
                            const int* kv_len_host, void* out_img, void* out_txt, int s_img,
                            int txt_rows, float scale, qie_stream_t stream);
 
+/* Same attention with the LAST 256-row query block of every (batch, head) computed as
+ * QIE_ATTN_SPLIT key ranges. Each range writes its fp32 partial (unnormalised O, row max, row
+ * sum) to `workspace`, then a combine kernel merges them. These blocks are dispatched after the
+ * others so they fill the grid's final, otherwise mostly idle, round. At 1024^2 there are
+ * 32 * 24 * B full blocks: a multiple of the 256 CUs. The split depends only on the block
+ * index, so every row's arithmetic is independent of the batch size.
+ * qie_attention_workspace_bytes returns the bytes needed in *bytes (0: no split for this
+ * shape); a workspace smaller than that returns QIE_ERR_INVALID. */
+#define QIE_ATTN_SPLIT 5
+int qie_attention_workspace_bytes(int batch, int heads, int s_pad, int s_img, int txt_rows,
+                                  int64_t* bytes);
+int qie_attention_fwd_split_bf16(const void* qkv, int batch, int heads, int s_pad,
+                                 const int* kv_len_host, void* out_img, void* out_txt, int s_img,
+                                 int txt_rows, float scale, void* workspace,
+                                 int64_t workspace_bytes, qie_stream_t stream);
+
 /* ------------------------------------------------------------------ small ops */
 
 /* K10 -- Timesteps(dim, flip_sin_to_cos=True, downscale_freq_shift=0,

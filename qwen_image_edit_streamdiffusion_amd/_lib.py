@@ -43,6 +43,8 @@ SIGNATURES = {
     "qie_rmsnorm_bf16": [P, P, P, I, I, F, P],
     "qie_qk_norm_rope_bf16": [P, I, I, I, I, I, I, P, P, P, P, F, P],
     "qie_attention_fwd_bf16": [P, I, I, I, IP, P, P, I, I, F, P],
+    "qie_attention_workspace_bytes": [I, I, I, I, I, POINTER(c_int64)],
+    "qie_attention_fwd_split_bf16": [P, I, I, I, IP, P, P, I, I, F, P, L, P],
     "qie_timestep_embed_bf16": [P, P, I, I, P],
     "qie_silu_bf16": [P, P, L, P],
     "qie_cfg_combine_bf16": [P, L, P, L, P, L, I, I, I, F, P],

@@ -9,19 +9,18 @@
 // the valid keys of batch row b are the prefix [0, kv_len[b]) -- key order does
 // not change softmax, RoPE was applied per token beforehand.
 //
-// Structure (gfx950): one workgroup = 8 waves = 256 query rows of one (b, h);
-// each wave owns 32 query rows.  Per 64-key tile:
-//   S^T = K . Q^T      (mfma 32x32x16 bf16, K rows by ds_read_b128 from an
-//                       XOR-swizzled LDS image, Q^T held in registers)
-//   -> each lane owns one query row: online softmax (running max / sum, exp2)
+// Structure (gfx950): one workgroup = 8 waves = 256 query rows of one (b, h), 32 rows per
+// wave, 64-key tiles:
+//   S^T = K . Q^T      (mfma 32x32x16 bf16, K rows by ds_read_b128 from an XOR-swizzled LDS
+//                       image, Q^T held in registers)
+//   -> each lane owns one query row: online softmax (running max / sum, exp2, lazy rescale T13)
 //      is lane-local except for one max exchange with the partner half-wave
 //   O^T += V^T . P^T   (the S^T accumulator registers ARE the P^T operand,
-//                       cdna_hip_programming.md §3 "accumulator as operand";
-//                       V^T fragments by ds_read_b64_tr_b16 with the matching
-//                       permuted key order)
-// K/V tiles are double buffered in LDS and register-staged: the next tile's
-// global loads are issued before the MFMAs and written after them (T14).
-// Workgroups of one (b, h) are placed on one XCD so its K/V stream from L2.
+//                       cdna_hip_programming.md §3 "accumulator as operand"; V^T fragments by
+//                       ds_read_b64_tr_b16 with the matching permuted key order)
+// scheduled as a two-group ping-pong (attn_pp_kernel below). Workgroups of one (b, h) share an
+// XCD so its K/V stream from L2; the last query block of every (b, h) can be split over the
+// key range into fp32 partials + a combine kernel (qie_attention_fwd_split_bf16).
 #include <type_traits>
 
 #include "qie_common.h"
@@ -40,6 +39,8 @@ struct AttnArgs {
   bf16_t* out_txt;
   int B, H, s_pad, s_img, txt_rows, qblocks;
   float c;  // scale * log2(e)
+  int split;  // key ranges of the last query block (0: none)
+  float* ws;  // split partials: O [B*H][split][256][128] fp32, then (m, l) [B*H][split][256][2]
   QieBatchI kv_len;
 };
 
@@ -48,193 +49,12 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
 }
 
-__global__ void __launch_bounds__(512) attn_fwd_kernel(AttnArgs a) {
-  __shared__ __attribute__((aligned(16))) char smem_raw[4 * kTileBytes];  // K0 V0 K1 V1
-  char QIE_LDS* smem = (char QIE_LDS*)smem_raw;
-
-  const int nwg = a.qblocks * a.H * a.B;
-  const int wgid = xcd_remap(blockIdx.x, nwg);
-  const int qb = wgid % a.qblocks;
-  const int bh = wgid / a.qblocks;
-  const int h = bh % a.H, b = bh / a.H;
-
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int hf = lane >> 5;   // half-wave
-  const int ql = lane & 31;   // query row within the wave / d column
-  const int64_t plane = (int64_t)a.s_pad * kDh;
-  const bf16_t* Qp = a.qkv + ((int64_t)(0 * a.B + b) * a.H + h) * plane;
-  const bf16_t* Kp = a.qkv + ((int64_t)(1 * a.B + b) * a.H + h) * plane;
-  const bf16_t* Vp = a.qkv + ((int64_t)(2 * a.B + b) * a.H + h) * plane;
-  const int kv_len = a.kv_len.v[b];
-  const int ntiles = (kv_len + kKB - 1) / kKB;
-
-  // ---- Q^T fragments (B operand): lane (q, hf) element j = Q[q][16ks + 8hf + j]
-  const int q_row = qb * kQB + wave * 32 + ql;
-  bf16x8_t qf[8];
-  {
-    const bf16_t* qr = Qp + (int64_t)q_row * kDh + 8 * hf;
-#pragma unroll
-    for (int ks = 0; ks < 8; ++ks) qf[ks] = *(const bf16x8_t*)(qr + 16 * ks);
-  }
-
-  // ---- staging: each thread moves 2 K chunks + 2 V chunks (16 B) per tile
-  u32x4_t stK[2], stV[2];
-  auto gload = [&](int t) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int id = tid + 512 * i;
-      const int row = id >> 4, ch = id & 15;
-      const int64_t off = (int64_t)(t * kKB + row) * kDh + ch * 8;
-      stK[i] = *(const u32x4_t*)(Kp + off);
-      stV[i] = *(const u32x4_t*)(Vp + off);
-    }
-  };
-  auto lwrite = [&](int buf) {
-    char QIE_LDS* kb = smem + buf * 2 * kTileBytes;
-    char QIE_LDS* vb = kb + kTileBytes;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int id = tid + 512 * i;
-      const int row = id >> 4, ch = id & 15;
-      *(u32x4_t QIE_LDS*)(kb + row * 256 + ((ch ^ (row & 15)) << 4)) = stK[i];
-      *(u32x4_t QIE_LDS*)(vb + row * 256 + ((ch ^ ((row & 3) << 2)) << 4)) = stV[i];
-    }
-  };
-
-  gload(0);
-  lwrite(0);
-  __syncthreads();
-  // Drain every outstanding load (Q fragments included) with a waitcnt the
-  // compiler's scoreboard sees: otherwise it keeps Q "pending" into the loop and
-  // waits on the in-order vmcnt there -- i.e. on the NEXT tile's prefetch,
-  // exposing the full global-load latency every tile.
-  __builtin_amdgcn_s_waitcnt(0);
-
-  f32x16_t o[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) o[i] = f32x16_t{};
-  float m_run = -INFINITY, l_run = 0.f;
-  const float c = a.c;
-
-  // per-lane LDS offsets
-  const int ksw = lane & 15;                        // K swizzle term (row & 15)
-  const int tri = lane & 15;                        // lane within 16-lane group
-  const int tr_row = (tri >> 2);                    // row within 4-row block
-  const int tr_sw = tr_row << 2;                    // V swizzle term ((row & 3) << 2)
-  const int tr_g1 = (lane >> 4) & 1;
-  const int tr_cb = 8 * (tri & 1);                  // byte within 16-B chunk
-
-  for (int t = 0; t < ntiles; ++t) {
-    const int cur = t & 1;
-    if (t + 1 < ntiles) gload(t + 1);
-    const char QIE_LDS* kb = smem + cur * 2 * kTileBytes;
-    const char QIE_LDS* vb = kb + kTileBytes;
-
-    // ---- S^T = K Q^T : two 32-key blocks
-    f32x16_t s[2];
-#pragma unroll
-    for (int cb = 0; cb < 2; ++cb) {
-      s[cb] = f32x16_t{};
-      const char QIE_LDS* krow = kb + (cb * 32 + ql) * 256;
-#pragma unroll
-      for (int ks = 0; ks < 8; ++ks) {
-        const bf16x8_t kf = *(const bf16x8_t QIE_LDS*)(krow + (((2 * ks + hf) ^ ksw) << 4));
-        s[cb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], s[cb], 0, 0, 0);
-      }
-    }
-    // ---- mask keys >= kv_len (only the last tile can contain them)
-    const int kv0 = t * kKB;
-    if (kv0 + kKB > kv_len) {
-#pragma unroll
-      for (int cb = 0; cb < 2; ++cb)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int kv = kv0 + cb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hf;
-          if (kv >= kv_len) s[cb][r] = -INFINITY;
-        }
-    }
-    // ---- online softmax (lane-local row; partner half holds the other 32 keys)
-    float mx = s[0][0];
-#pragma unroll
-    for (int r = 1; r < 16; ++r) mx = fmaxf(mx, s[0][r]);
-#pragma unroll
-    for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[1][r]);
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    // lazy rescale (cdna_hip_programming.md T13): keep the running max unless a
-    // row of this wave grows by more than kRescaleThr (log2 units); P is then
-    // bounded by 2^kRescaleThr.  The decision covers this tile before any of its
-    // P is formed, and the previous tile's P.V is complete.
-    if (__any((mx - m_run) * c > kRescaleThr)) {
-      const float m_new = fmaxf(m_run, mx);
-      const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * c);
-      m_run = m_new;
-      l_run *= alpha;
-#pragma unroll
-      for (int db = 0; db < 4; ++db) o[db] *= alpha;
-    }
-    const float mc = m_run * c;
-    float psum = 0.f;
-    bf16x8_t pf[4];
-#pragma unroll
-    for (int cb = 0; cb < 2; ++cb)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[cb][r], c, -mc));
-        psum += p;
-        pf[cb * 2 + (r >> 3)][r & 7] = (__bf16)p;
-      }
-    l_run += psum;
-
-    // ---- O^T += V^T P^T
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      const int r0 = 16 * ks + 4 * hf + tr_row;   // rows r0 and r0 + 8
-#pragma unroll
-      for (int db = 0; db < 4; ++db) {
-        const int chunk = (4 * db + 2 * tr_g1 + ((tri & 3) >> 1)) ^ tr_sw;
-        const char QIE_LDS* p0 = vb + r0 * 256 + (chunk << 4) + tr_cb;
-        const s16x4_t va = __builtin_amdgcn_ds_read_tr16_b64_v4i16((s16x4_t QIE_LDS*)p0);
-        const s16x4_t vb2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((s16x4_t QIE_LDS*)(p0 + 8 * 256));
-        typedef __attribute__((ext_vector_type(8))) short s16x8_t;
-        const s16x8_t vv = __builtin_shufflevector(va, vb2, 0, 1, 2, 3, 4, 5, 6, 7);
-        o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, vv), pf[ks],
-                                                        o[db], 0, 0, 0);
-      }
-    }
-    if (t + 1 < ntiles) lwrite(cur ^ 1);
-    __syncthreads();
-  }
-
-  // ---- normalise and store: lane (q, hf) holds d = 32db + 8g + 4hf + (0..3)
-  const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
-  const float inv = 1.0f / l_tot;
-  const int s = q_row;
-  bf16_t* dst = nullptr;
-  if (s < a.s_img) {
-    dst = a.out_img + ((int64_t)b * a.s_img + s) * (a.H * kDh) + h * kDh;
-  } else if (s < a.s_img + a.txt_rows) {
-    dst = a.out_txt + ((int64_t)b * a.txt_rows + (s - a.s_img)) * (a.H * kDh) + h * kDh;
-  }
-  if (dst) {
-#pragma unroll
-    for (int db = 0; db < 4; ++db)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int d = 32 * db + 8 * g + 4 * hf;
-        const u32x2_t w = {pack2(o[db][4 * g] * inv, o[db][4 * g + 1] * inv),
-                           pack2(o[db][4 * g + 2] * inv, o[db][4 * g + 3] * inv)};
-        *(u32x2_t*)(dst + d) = w;
-      }
-  }
-}
-
 // =============================================================================================
-// Ping-pong variant (attn_pp_kernel). Same math, lane layout and LDS swizzles as
-// attn_fwd_kernel; only the schedule differs. Waves 0-3 (group 0) and 4-7 (group 1) put one
+// attn_pp_kernel. Waves 0-3 (group 0) and 4-7 (group 1) put one
 // wave of each group on every SIMD. Group 1 runs one phase behind group 0, so while one wave
 // of a SIMD is in its MFMA phase the other is in its VALU phase:
 //   M-phase t : S(t) = K(t) Q^T (16 MFMA) then O += V(t-1)^T P(t-1)^T (16 MFMA), operands
-//               streamed from LDS three MFMAs ahead;
+//               streamed from LDS five MFMAs ahead, at raised issue priority;
 //   V-phase t : masking, online softmax of S(t) -> P(t) (bf16), lazy O rescale, and the
 //               LDS-DMA of K(t+2) / V(t+1).
 // The MFMAs are asm volatile (their order and the LDS reads between them stay as written) and
@@ -303,10 +123,21 @@ __global__ void __launch_bounds__(512) attn_pp_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) char smem_raw[2 * kRing * kTileBytes];  // K ring, V ring
   char QIE_LDS* smem = (char QIE_LDS*)smem_raw;
 
-  const int nwg = a.qblocks * a.H * a.B;
-  const int wgid = xcd_remap(blockIdx.x, nwg);
-  const int qb = wgid % a.qblocks;
-  const int bh = wgid / a.qblocks;
+  // blocks [0, nfull): whole query blocks (XCD-grouped per (b, h)); then, if split, the last
+  // query block of every (b, h) as `split` key ranges -- dispatched last, filling the final round
+  const int qbf = a.split ? a.qblocks - 1 : a.qblocks;
+  const int nfull = qbf * a.H * a.B;
+  int qb, bh, chunk = -1;
+  if ((int)blockIdx.x < nfull) {
+    const int wgid = xcd_remap(blockIdx.x, nfull);
+    qb = wgid % qbf;
+    bh = wgid / qbf;
+  } else {
+    const int j = blockIdx.x - nfull;
+    bh = j / a.split;
+    chunk = j - bh * a.split;
+    qb = a.qblocks - 1;
+  }
   const int h = bh % a.H, b = bh / a.H;
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -319,7 +150,10 @@ __global__ void __launch_bounds__(512) attn_pp_kernel(AttnArgs a) {
   const bf16_t* Kp = a.qkv + ((int64_t)(1 * a.B + b) * a.H + h) * plane;
   const bf16_t* Vp = a.qkv + ((int64_t)(2 * a.B + b) * a.H + h) * plane;
   const int kv_len = a.kv_len.v[b];
-  const int ntiles = (kv_len + kKB - 1) / kKB;
+  const int ntot = (kv_len + kKB - 1) / kKB;
+  // key tiles [t0, ntiles) of this work-group
+  const int t0 = chunk < 0 ? 0 : chunk * ntot / a.split;
+  const int ntiles = chunk < 0 ? ntot : (chunk + 1) * ntot / a.split;
 
   PPState st;
 #ifdef QIE_ATTN_STAMP
@@ -354,7 +188,7 @@ __global__ void __launch_bounds__(512) attn_pp_kernel(AttnArgs a) {
     for (int p = 0; p < 2; ++p) attn_dma(vr, base + (wave + 8 * p) * 1024, vo[p], t * kTileBytes);
   };
 
-  // per-lane LDS read offsets (as attn_fwd_kernel)
+  // per-lane LDS read offsets (K: chunk ^ (row & 15); V: transposed 4x16 reads, chunk ^ ((row & 3) << 2))
   const int ksw = lane & 15;
   const int tri = lane & 15;
   const int tr_row = tri >> 2;
@@ -377,7 +211,6 @@ __global__ void __launch_bounds__(512) attn_pp_kernel(AttnArgs a) {
     const char QIE_LDS* p0 = vb + r0 * 256 + (chunk << 4) + tr_cb;
     const s16x4_t va = __builtin_amdgcn_ds_read_tr16_b64_v4i16((s16x4_t QIE_LDS*)p0);
     const s16x4_t vb2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((s16x4_t QIE_LDS*)(p0 + 8 * 256));
-    typedef __attribute__((ext_vector_type(8))) short s16x8_t;
     return __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(va, vb2, 0, 1, 2, 3, 4, 5, 6, 7));
   };
   auto mfma_i = [&](int i, const bf16x8_t& A) {
@@ -390,27 +223,20 @@ __global__ void __launch_bounds__(512) attn_pp_kernel(AttnArgs a) {
       mma32(st.o[j & 3], A, st.pf[j >> 2]);
     }
   };
-  // M-phase over MFMAs [i0, i1): operands prefetched three MFMAs ahead
-  auto mphase = [&](auto i0_t, auto i1_t, int tk, int tv, int td) {
+  // M-phase over MFMAs [i0, i1): operands prefetched PF MFMAs ahead
+  auto mphase = [&](auto i0_t, auto i1_t, int tk, int tv) {
     constexpr int i0 = decltype(i0_t)::value, i1 = decltype(i1_t)::value;
-    const bool dk = td >= 0 && td + 2 < ntiles, dv = td >= 0 && td + 1 < ntiles;
-    bf16x8_t A[4];
+    constexpr int PF = 5;  // operand prefetch distance in MFMAs (3: -0.7 %, 7: -0.3 %)
+    bf16x8_t A[8];
     // the MFMA wave outranks its SIMD partner (in its softmax phase) for issue: otherwise the
     // older wave group wins arbitration and starves the younger group's MFMA phase
     __builtin_amdgcn_s_setprio(2);
 #pragma unroll
-    for (int i = i0; i < i0 + 3 && i < i1; ++i) A[i & 3] = opA(i, tk, tv);
+    for (int i = i0; i < i0 + PF && i < i1; ++i) A[i & 7] = opA(i, tk, tv);
 #pragma unroll
     for (int i = i0; i < i1; ++i) {
-      if (i + 3 < i1) A[(i + 3) & 3] = opA(i + 3, tk, tv);
-      mfma_i(i, A[i & 3]);
-#ifdef QIE_ATTN_DMA_M
-      // this phase's LDS-DMA pieces, one after every 8th MFMA: K(td+2) rows, then V(td+1)
-      if (i - i0 == 4 && dk) attn_dma(kr, smem + ((td + 2) % kRing) * kTileBytes + wave * 1024, ko[0], (td + 2) * kTileBytes);
-      if (i - i0 == 12 && dk) attn_dma(kr, smem + ((td + 2) % kRing) * kTileBytes + (wave + 8) * 1024, ko[1], (td + 2) * kTileBytes);
-      if (i - i0 == 20 && dv) attn_dma(vr, smem + (kRing + (td + 1) % kRing) * kTileBytes + wave * 1024, vo[0], (td + 1) * kTileBytes);
-      if (i - i0 == 28 && dv) attn_dma(vr, smem + (kRing + (td + 1) % kRing) * kTileBytes + (wave + 8) * 1024, vo[1], (td + 1) * kTileBytes);
-#endif
+      if (i + PF < i1) A[(i + PF) & 7] = opA(i + PF, tk, tv);
+      mfma_i(i, A[i & 7]);
     }
     __builtin_amdgcn_s_setprio(0);
   };
@@ -421,10 +247,8 @@ __global__ void __launch_bounds__(512) attn_pp_kernel(AttnArgs a) {
 #pragma unroll
     for (int db = 0; db < 4; ++db) rfence(st.o[db]);
     int pieces = 0;
-#ifndef QIE_ATTN_DMA_M
     if (t + 2 < ntiles) { dmaK(t + 2); pieces += 2; }
     if (t + 1 < ntiles) { dmaV(t + 1); pieces += 2; }
-#endif
     const int kv0 = t * kKB;
     if (kv0 + kKB > kv_len) {
 #pragma unroll
@@ -478,11 +302,21 @@ __global__ void __launch_bounds__(512) attn_pp_kernel(AttnArgs a) {
   using I0 = std::integral_constant<int, 0>;
   using I16 = std::integral_constant<int, 16>;
   using I32 = std::integral_constant<int, 32>;
+  using IMEND = I32;
 
-  // ---- prologue: K(0), K(1), V(0) resident; group 1 waits one phase
-  dmaK(0);
-  if (ntiles > 1) dmaK(1);
-  dmaV(0);
+  const int q_loc = wave * 32 + ql;  // row within the query block
+  if (t0 >= ntiles) {                // empty key range (fewer tiles than ranges): neutral partial
+    float* po = a.ws + (((int64_t)bh * a.split + chunk) * kQB + q_loc) * kDh;
+    float* pml = a.ws + (int64_t)a.B * a.H * a.split * kQB * kDh;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) *(f32x4_t*)(po + 8 * k + 4 * hf) = f32x4_t{0, 0, 0, 0};
+    if (hf == 0) *(f32x2_t*)(pml + (((int64_t)bh * a.split + chunk) * kQB + q_loc) * 2) = f32x2_t{-INFINITY, 0.f};
+    return;
+  }
+  // ---- prologue: K(t0), K(t0+1), V(t0) resident; group 1 waits one phase
+  dmaK(t0);
+  if (t0 + 1 < ntiles) dmaK(t0 + 1);
+  dmaV(t0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the asm DMA pieces
   __builtin_amdgcn_s_waitcnt(0);                     // Q fragments (hipcc-tracked)
   asm volatile("s_barrier" ::: "memory");
@@ -492,23 +326,13 @@ __global__ void __launch_bounds__(512) attn_pp_kernel(AttnArgs a) {
   st.m_run = -INFINITY;
   st.l_run = 0.f;
 
-#ifdef QIE_ATTN_DMA_M
-  // pieces issued in M-phase t stay in flight across its barrier; V-phase t ends with vmcnt(0)
-  auto mend = [&](int t) {
-    const int n = (t + 2 < ntiles ? 2 : 0) + (t + 1 < ntiles ? 2 : 0);
-    if (n == 4) asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
-    else if (n == 2) asm volatile("s_waitcnt vmcnt(2)\n\ts_barrier" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-  };
-#else
   auto mend = [&](int) { asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory"); };
-#endif
-  mphase(I0{}, I16{}, 0, 0, 0);  // S(0)  (DMA of K(2), V(1) when issued in M-phases)
-  mend(0);
-  vphase(0);
-  for (int t = 1; t < ntiles; ++t) {
+  mphase(I0{}, I16{}, t0, t0);  // S(t0)
+  mend(t0);
+  vphase(t0);
+  for (int t = t0 + 1; t < ntiles; ++t) {
     STAMP(t0);
-    mphase(I0{}, I32{}, t, t - 1, t);  // S(t), O += V(t-1) P(t-1)
+    mphase(I0{}, IMEND{}, t, t - 1);  // S(t), O += V(t-1) P(t-1)
     STAMP(t1);
     mend(t);
     STAMP(t2);
@@ -523,12 +347,23 @@ __global__ void __launch_bounds__(512) attn_pp_kernel(AttnArgs a) {
   if (lane == 0)
     for (int i = 0; i < 4; ++i) atomicAdd(&g_stamp[grp][i], acc_st[i]);
 #endif
-  mphase(I16{}, I32{}, 0, ntiles - 1, -1);  // O += V(T-1) P(T-1)
+  mphase(I16{}, IMEND{}, t0, ntiles - 1);  // O += V(T-1) P(T-1)
   if (grp == 0) asm volatile("s_barrier" ::: "memory");
   // MFMA D -> VALU read hazard before the epilogue reads O (asm MFMAs are not padded by hipcc)
   asm volatile("s_nop 15\n\ts_nop 7" : "+v"(st.o[0]), "+v"(st.o[1]), "+v"(st.o[2]), "+v"(st.o[3]));
-
   const float l_tot = st.l_run + __shfl_xor(st.l_run, 32, 64);
+  if (chunk >= 0) {  // fp32 partial: unnormalised O (d = 32db + 8g + 4hf + 0..3), row max, row sum
+    float* po = a.ws + (((int64_t)bh * a.split + chunk) * kQB + q_loc) * kDh;
+    float* pml = a.ws + (int64_t)a.B * a.H * a.split * kQB * kDh;
+#pragma unroll
+    for (int db = 0; db < 4; ++db)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        *(f32x4_t*)(po + 32 * db + 8 * g + 4 * hf) =
+            f32x4_t{st.o[db][4 * g], st.o[db][4 * g + 1], st.o[db][4 * g + 2], st.o[db][4 * g + 3]};
+    if (hf == 0) *(f32x2_t*)(pml + (((int64_t)bh * a.split + chunk) * kQB + q_loc) * 2) = f32x2_t{st.m_run, l_tot};
+    return;
+  }
   const float inv = 1.0f / l_tot;
   const int s = q_row;
   bf16_t* dst = nullptr;
@@ -550,16 +385,46 @@ __global__ void __launch_bounds__(512) attn_pp_kernel(AttnArgs a) {
   }
 }
 
+// Merges the `split` partials of the last query block: O = sum_c w_c O_c / sum_c w_c l_c with
+// w_c = exp2((m_c - max_c m_c) * c). One wave per (b, h, row), two d values per lane.
+__global__ void __launch_bounds__(256) attn_combine_kernel(AttnArgs a) {
+  const int wid = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (wid >= a.B * a.H * kQB) return;
+  const int bh = wid / kQB, r = wid - bh * kQB;
+  const int h = bh % a.H, b = bh / a.H;
+  const int s = (a.qblocks - 1) * kQB + r;
+  bf16_t* dst = nullptr;
+  if (s < a.s_img) dst = a.out_img + ((int64_t)b * a.s_img + s) * (a.H * kDh) + h * kDh;
+  else if (s < a.s_img + a.txt_rows)
+    dst = a.out_txt + ((int64_t)b * a.txt_rows + (s - a.s_img)) * (a.H * kDh) + h * kDh;
+  if (!dst) return;
+  const float* pml = a.ws + (int64_t)a.B * a.H * a.split * kQB * kDh;
+  float mx = -INFINITY;
+  for (int c = 0; c < a.split; ++c) mx = fmaxf(mx, pml[(((int64_t)bh * a.split + c) * kQB + r) * 2]);
+  float l = 0.f, o0 = 0.f, o1 = 0.f;
+  for (int c = 0; c < a.split; ++c) {
+    const int64_t pi = ((int64_t)bh * a.split + c) * kQB + r;
+    const float mc = pml[pi * 2], lc = pml[pi * 2 + 1];
+    const float w = mc == -INFINITY ? 0.f : __builtin_amdgcn_exp2f((mc - mx) * a.c);
+    const f32x2_t ov = *(const f32x2_t*)(a.ws + pi * kDh + 2 * lane);
+    l += w * lc;
+    o0 += w * ov[0];
+    o1 += w * ov[1];
+  }
+  const float inv = 1.0f / l;
+  *(uint32_t*)(dst + 2 * lane) = pack2(o0 * inv, o1 * inv);
+}
+
 }  // namespace
 
-extern "C" int qie_attention_fwd_bf16(const void* qkv, int batch, int heads, int s_pad,
-                                      const int* kv_len_host, void* out_img, void* out_txt,
-                                      int s_img, int txt_rows, float scale, qie_stream_t stream) {
+namespace {
+int attn_args(AttnArgs& a, const void* qkv, int batch, int heads, int s_pad, const int* kv_len_host,
+              void* out_img, void* out_txt, int s_img, int txt_rows, float scale) {
   QIE_CHECK_ARG(qkv && kv_len_host && out_img && (out_txt || txt_rows == 0));
   QIE_CHECK_ARG(batch > 0 && batch <= QIE_MAX_BATCH && heads > 0);
   QIE_CHECK_ARG(s_pad > 0 && s_pad % kQB == 0 && s_img >= 0 && txt_rows >= 0);
-  QIE_CHECK_ARG(s_img + txt_rows <= s_pad);
-  AttnArgs a{};
+  QIE_CHECK_ARG(s_img + txt_rows <= s_pad && s_img + txt_rows > 0);
+  a = AttnArgs{};
   a.qkv = (const bf16_t*)qkv;
   a.out_img = (bf16_t*)out_img;
   a.out_txt = (bf16_t*)out_txt;
@@ -574,11 +439,49 @@ extern "C" int qie_attention_fwd_bf16(const void* qkv, int batch, int heads, int
     QIE_CHECK_ARG(kv_len_host[i] > 0 && kv_len_host[i] <= s_pad);
     a.kv_len.v[i] = kv_len_host[i];
   }
-  const int nwg = a.qblocks * heads * batch;
-#ifdef QIE_ATTN_PP
-  attn_pp_kernel<<<nwg, 512, 0, (hipStream_t)stream>>>(a);
-#else
-  attn_fwd_kernel<<<nwg, 512, 0, (hipStream_t)stream>>>(a);
-#endif
+  return QIE_OK;
+}
+
+int64_t split_bytes(int batch, int heads, int qblocks) {
+  return qblocks > 1 ? (int64_t)batch * heads * QIE_ATTN_SPLIT * kQB * (kDh + 2) * 4 : 0;
+}
+}  // namespace
+
+extern "C" int qie_attention_fwd_bf16(const void* qkv, int batch, int heads, int s_pad,
+                                      const int* kv_len_host, void* out_img, void* out_txt,
+                                      int s_img, int txt_rows, float scale, qie_stream_t stream) {
+  AttnArgs a;
+  const int rc = attn_args(a, qkv, batch, heads, s_pad, kv_len_host, out_img, out_txt, s_img, txt_rows, scale);
+  if (rc) return rc;
+  attn_pp_kernel<<<a.qblocks * heads * batch, 512, 0, (hipStream_t)stream>>>(a);
+  return qie_last_error();
+}
+
+extern "C" int qie_attention_workspace_bytes(int batch, int heads, int s_pad, int s_img, int txt_rows,
+                                             int64_t* bytes) {
+  QIE_CHECK_ARG(bytes && batch > 0 && heads > 0 && s_pad > 0 && s_img >= 0 && txt_rows >= 0);
+  *bytes = split_bytes(batch, heads, (s_img + txt_rows + kQB - 1) / kQB);
+  return QIE_OK;
+}
+
+extern "C" int qie_attention_fwd_split_bf16(const void* qkv, int batch, int heads, int s_pad,
+                                            const int* kv_len_host, void* out_img, void* out_txt,
+                                            int s_img, int txt_rows, float scale, void* workspace,
+                                            int64_t workspace_bytes, qie_stream_t stream) {
+  AttnArgs a;
+  const int rc = attn_args(a, qkv, batch, heads, s_pad, kv_len_host, out_img, out_txt, s_img, txt_rows, scale);
+  if (rc) return rc;
+  const int64_t need = split_bytes(batch, heads, a.qblocks);
+  const hipStream_t s = (hipStream_t)stream;
+  if (need == 0) {  // a single query block: nothing to split
+    attn_pp_kernel<<<a.qblocks * heads * batch, 512, 0, s>>>(a);
+    return qie_last_error();
+  }
+  QIE_CHECK_ARG(workspace && workspace_bytes >= need && ((uintptr_t)workspace % 16) == 0);
+  a.split = QIE_ATTN_SPLIT;
+  a.ws = (float*)workspace;
+  const int grid = ((a.qblocks - 1) + a.split) * heads * batch;
+  attn_pp_kernel<<<grid, 512, 0, s>>>(a);
+  attn_combine_kernel<<<(batch * heads * kQB + 3) / 4, 256, 0, s>>>(a);
   return qie_last_error();
 }

@@ -162,9 +162,18 @@ def quantize_rows(x: torch.Tensor, q: torch.Tensor, scale: torch.Tensor):
 
 
 # ---------------------------------------------------------------------------- attention
+def attention_workspace_bytes(B: int, H: int, S_pad: int, s_img: int, txt_rows: int) -> int:
+    """Bytes of the split-key workspace ``attention(..., workspace=)`` uses (0: no split)."""
+    n = ctypes.c_int64(0)
+    _lib.call("qie_attention_workspace_bytes", B, H, S_pad, s_img, txt_rows, ctypes.byref(n))
+    return n.value
+
+
 def attention(qkv: torch.Tensor, kv_len: Sequence[int], out_img: torch.Tensor,
               out_txt: Optional[torch.Tensor], s_img: int, txt_rows: int,
-              scale: Optional[float] = None) -> None:
+              scale: Optional[float] = None, workspace: Optional[torch.Tensor] = None) -> None:
+    """Joint attention. With ``workspace`` (>= attention_workspace_bytes) the last query block
+    of every (b, h) is split over the key range (qie_attention_fwd_split_bf16)."""
     _dev(qkv, out_img, out_txt)
     _, B, H, S_pad, Dh = qkv.shape
     _chk(Dh == 128 and S_pad % 256 == 0 and len(kv_len) == B and B <= 16, "attention shapes")
@@ -174,8 +183,13 @@ def attention(qkv: torch.Tensor, kv_len: Sequence[int], out_img: torch.Tensor,
     _chk(all(0 < k <= S_pad for k in kv_len), "kv_len")
     arr = (ctypes.c_int * B)(*[int(k) for k in kv_len])
     sc = 1.0 / math.sqrt(Dh) if scale is None else scale
-    _lib.call("qie_attention_fwd_bf16", _p(qkv), B, H, S_pad, arr, _p(out_img), _p(out_txt), s_img,
-              txt_rows, sc, _stream())
+    if workspace is None:
+        _lib.call("qie_attention_fwd_bf16", _p(qkv), B, H, S_pad, arr, _p(out_img), _p(out_txt), s_img,
+                  txt_rows, sc, _stream())
+    else:
+        _dev(workspace)
+        _lib.call("qie_attention_fwd_split_bf16", _p(qkv), B, H, S_pad, arr, _p(out_img), _p(out_txt),
+                  s_img, txt_rows, sc, _p(workspace), workspace.numel() * workspace.element_size(), _stream())
 
 
 # ---------------------------------------------------------------------------- small ops

@@ -106,6 +106,9 @@ class _Workspace:
         self.mlp_img = torch.empty(R_i, F, **e)
         self.mlp_txt = torch.empty(max(R_t, 1), F, **e)
         self.qkv = torch.zeros(3, B, H, self.S_pad, Dh, **e)  # pad rows stay 0 (finite V)
+        # fp32 partials of the key-split last query block of every (b, h) (attention tail)
+        nb = ops.attention_workspace_bytes(B, H, self.S_pad, S_img, S_txt)
+        self.attn_split = torch.empty(max(nb // 4, 4), device=device, dtype=torch.float32)
         # split-K partial sums of the text-stream linears (fp32 / int32)
         sk = max(ops.splitk_splits(n, k, int8) * n for n, k in ((3 * D, D), (D, D), (F, D), (D, F)))
         self.splitk = torch.empty(max(R_t * sk, 4), device=device, dtype=torch.float32)
@@ -489,7 +492,8 @@ class QwenImageTransformer2DModel(nn.Module):
         if has_txt:
             ops.qk_norm_rope(ws.qkv, S_img, S_txt, blk.norm_added_q, blk.norm_added_k, tcos, tsin, eps)
         with self._probe("attention"):
-            ops.attention(ws.qkv, kv_len, ws.att_img, ws.att_txt[:R_t] if has_txt else None, S_img, S_txt)
+            ops.attention(ws.qkv, kv_len, ws.att_img, ws.att_txt[:R_t] if has_txt else None, S_img, S_txt,
+                          workspace=ws.attn_split)
         # ---- out-proj + gated residual, LN2 + modulate, MLP + gated residual
         for s, x, h, att, mlp, m, rpb, seq_off in streams:
             if i8:

@@ -77,3 +77,11 @@ def test_invalid_arguments_rejected_on_host(lib):
     assert lib.qie_linear_splitk_bf16(16, 256, 16, 16, ep, 8, 256, 192, 2, 16, 1 << 20, None) == -1
     assert lib.qie_linear_splitk_bf16(16, 256, 16, 16, ep, 8, 256, 256, 2, 16, 8 * 256 * 4, None) == -1
     assert lib.qie_linear_splitk_i8(16, 256, None, 16, 16, 16, ep, 8, 256, 256, 2, 16, 1 << 20, None) == -1
+    # attention workspace query (host only) and the split entry's workspace check
+    n = ctypes.c_int64(-1)
+    assert lib.qie_attention_workspace_bytes(2, 24, 8448, 8192, 216, ctypes.byref(n)) == 0
+    assert n.value == 2 * 24 * 5 * 256 * 130 * 4
+    assert lib.qie_attention_workspace_bytes(1, 1, 256, 200, 0, ctypes.byref(n)) == 0 and n.value == 0
+    assert lib.qie_attention_workspace_bytes(1, 1, 256, 200, 0, None) == -1
+    kv = (ctypes.c_int * 1)(512)
+    assert lib.qie_attention_fwd_split_bf16(16, 1, 1, 512, kv, 16, None, 512, 0, 0.1, None, 0, None) == -1

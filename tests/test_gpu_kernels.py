@@ -188,6 +188,45 @@ def test_attention(dev, B, H, s_img, txt_rows, kv_len, scale):
         close(ot[: B * txt_rows], rt, rel_l2=1e-2, ulps=8)
 
 
+@pytest.mark.parametrize("B,H,s_img,txt_rows,kv_len", [
+    (1, 2, 512, 40, [552]),            # 3 query blocks, last one split over 9 key tiles
+    (2, 3, 1024, 216, [1240, 1100]),   # masked keys in a middle range of row 1
+    (1, 1, 256, 20, [100]),            # 2 key tiles < 5 ranges: empty ranges combine to nothing
+    (1, 1, 256, 0, [256]),             # one query block: nothing to split
+])
+def test_attention_split_tail(dev, B, H, s_img, txt_rows, kv_len):
+    """qie_attention_fwd_split_bf16: the last query block of each (b, h) as key ranges + combine;
+    same tolerance as the unsplit kernel vs the oracle, and close to the unsplit result."""
+    ops = _ops()
+    s_pad = ((s_img + txt_rows + 255) // 256) * 256
+    qkv = rnd((3, B, H, s_pad, 128), dev, 1.0, 33)
+    qkv[:, :, :, s_img + txt_rows:] = 0
+    nb = ops.attention_workspace_bytes(B, H, s_pad, s_img, txt_rows)
+    assert (nb > 0) == (s_pad > 256)
+    ws = torch.full((max(nb // 4, 4),), float("nan"), device=dev)  # stale data must not leak
+    outs = []
+    for w in (ws, None):
+        oi = torch.empty(B * s_img, H * 128, dtype=BF16, device=dev)
+        ot = torch.empty(max(B * txt_rows, 1), H * 128, dtype=BF16, device=dev)
+        ops.attention(qkv, kv_len, oi, ot[: B * txt_rows] if txt_rows else None, s_img, txt_rows, workspace=w)
+        outs.append((oi, ot[: B * txt_rows]))
+    ri, rt = _attn_ref(qkv, kv_len, s_img, txt_rows)
+    close(outs[0][0], ri, rel_l2=1e-2, ulps=8)
+    close(outs[0][0], outs[1][0], rel_l2=4e-3, ulps=4)
+    if txt_rows:
+        close(outs[0][1], rt, rel_l2=1e-2, ulps=8)
+
+
+def test_attention_split_workspace_too_small(dev):
+    from qwen_image_edit_streamdiffusion_amd import _lib
+    ops = _ops()
+    qkv = rnd((3, 1, 1, 512, 128), dev, 1.0, 34)
+    oi = torch.empty(512, 128, dtype=BF16, device=dev)
+    ws = torch.empty(16, device=dev)
+    with pytest.raises(_lib.QieError):
+        ops.attention(qkv, [512], oi, None, 512, 0, workspace=ws)
+
+
 def test_attention_spike_rescale(dev):
     """Force the online-softmax rescale: one key far above the rest in a late tile."""
     ops = _ops()

@@ -21,6 +21,9 @@ def load(path):
     lib.qie_attention_fwd_bf16.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                            ctypes.POINTER(ctypes.c_int), ctypes.c_void_p, ctypes.c_void_p,
                                            ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_void_p]
+    if hasattr(lib, "qie_attention_fwd_split_bf16"):
+        lib.qie_attention_fwd_split_bf16.argtypes = lib.qie_attention_fwd_bf16.argtypes[:-1] + [
+            ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
     lib.qie_linear_bf16.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
                                     ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                     ctypes.c_int, ctypes.c_void_p]
@@ -35,7 +38,7 @@ def main():
     libs = [load(p) for p in paths]
     dev = torch.device("cuda:0")
     st = torch.cuda.current_stream().cuda_stream
-    if what == "attention":
+    if what in ("attention", "attention_nosplit"):
         B, H, S_IMG, S_TXT = 2, 24, 8192, 216
         S = S_IMG + S_TXT
         s_pad = ((S + 255) // 256) * 256
@@ -46,8 +49,16 @@ def main():
         kv = (ctypes.c_int * B)(*[S] * B)
         flops = 4.0 * B * S * S * H * 128
 
+        ws = torch.empty(B * H * 5 * 256 * 130, device=dev)  # QIE_ATTN_SPLIT = 5
+
         def run(i):
-            rc = libs[i].qie_attention_fwd_bf16(qkv.data_ptr(), B, H, s_pad, kv, outs[i][0].data_ptr(),
+            lib = libs[i]
+            if what == "attention" and hasattr(lib, "qie_attention_fwd_split_bf16"):
+                rc = lib.qie_attention_fwd_split_bf16(qkv.data_ptr(), B, H, s_pad, kv, outs[i][0].data_ptr(),
+                                                      outs[i][1].data_ptr(), S_IMG, S_TXT, 1 / math.sqrt(128),
+                                                      ws.data_ptr(), ws.numel() * 4, st)
+            else:
+                rc = lib.qie_attention_fwd_bf16(qkv.data_ptr(), B, H, s_pad, kv, outs[i][0].data_ptr(),
                                                 outs[i][1].data_ptr(), S_IMG, S_TXT, 1 / math.sqrt(128), st)
             assert rc == 0, rc
     elif what.startswith("gemm"):

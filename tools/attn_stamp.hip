@@ -1,6 +1,6 @@
 // Diagnostic harness (not part of the product): builds the ping-pong attention kernel with
 // s_memtime stamps around its phases and prints average cycles per tile per group.
-//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -DQIE_ATTN_PP -DQIE_ATTN_STAMP -Iinclude \
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -DQIE_ATTN_STAMP -Iinclude \
 //         tools/attn_stamp.hip -o tools/attn_stamp && ./tools/attn_stamp
 #include <cstdio>
 #include <cstdlib>
