@@ -26,6 +26,8 @@ restatement on the host cores, bounded sample (see cpu_baseline()).
 from __future__ import annotations
 
 import argparse
+import contextlib
+import ctypes
 import json
 import os
 import sys
@@ -73,6 +75,21 @@ def cpu_baseline(budget_note: str = ""):
             "sec_per_image": sec_per_image}
 
 
+@contextlib.contextmanager
+def _stdout_to_stderr():
+    """Route C-level writes to fd 1 (library banners) to stderr for the duration."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        yield
+    finally:
+        ctypes.CDLL(None).fflush(None)  # C stdio buffers go out while fd 1 is still stderr
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -82,6 +99,9 @@ def main():
     ap.add_argument("--layers", type=int, default=60, help="debug only; the headline needs 60")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-probe", action="store_true")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="debug: run the collective path (process group, broadcast, gather, "
+                         "barriers, max-reduce) even at world size 1")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -89,8 +109,13 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+    dist_on = world > 1 or args.force_dist
+    if dist_on:
+        # RCCL prints a version banner on stdout when the communicator is created; stdout must
+        # carry only the one JSON line, so fd 1 points at stderr until the first barrier is done
+        with _stdout_to_stderr():
+            dist.init_process_group("nccl", device_id=dev)
+            dist.barrier()
 
     from qwen_image_edit_streamdiffusion_amd import (QwenImageTransformer2DModel, StreamBatchDenoiser,
                                                      QwenImageEditPlusPipeline)
@@ -105,7 +130,7 @@ def main():
     # ---- synthetic inputs, resident in HBM before timing
     g = torch.Generator(device=dev).manual_seed(44)
     pe = torch.randn(1, S_TXT, 3584, generator=g, device=dev, dtype=BF16)
-    if world > 1:
+    if dist_on:
         dist.broadcast(pe, 0)  # prompt-embed cache filled once, from rank 0
     gr = torch.Generator(device=dev).manual_seed(1000 + rank)
     nf = 8
@@ -139,11 +164,11 @@ def main():
                         output_type="latent").images
 
     gather_buf = None
-    if world > 1 and rank == 0:
+    if dist_on and rank == 0:
         gather_buf = [torch.empty(1, S_NOISE, 64, dtype=BF16, device=dev) for _ in range(world)]
 
     def deliver(res):
-        if world > 1:
+        if dist_on:
             lat = res[1] if isinstance(res, tuple) else res
             dist.gather(lat, gather_buf if rank == 0 else None, dst=0)
 
@@ -156,7 +181,7 @@ def main():
     torch.cuda.synchronize()
     if not args.no_probe:
         model.probe = {k: [] for k in probe_keys}
-    if world > 1:
+    if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.time()
@@ -167,10 +192,10 @@ def main():
             done += 1
             deliver(r)
     torch.cuda.synchronize()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     el = time.time() - t0
-    if world > 1:
+    if dist_on:
         tt = torch.tensor([el], device=dev, dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         el = tt.item()
@@ -248,7 +273,7 @@ def main():
             "roofline": roof, "kernels": kernels, "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if dist_on:
         dist.destroy_process_group()
 
 

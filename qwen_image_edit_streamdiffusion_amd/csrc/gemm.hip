@@ -323,10 +323,22 @@ __global__ void __launch_bounds__(WM* WN * 64)
 constexpr int k4RowBytes = 64;
 constexpr int k4Tile = 256 * k4RowBytes;  // one operand slice, 16 KiB
 constexpr int k4Stage = 2 * k4Tile;       // X + W slice, 32 KiB
-constexpr int k4Slots = 4;
+#ifndef QIE_RING_DEPTH  // 4 (5 slots, 160 KiB) measured -1 % vs 3
+#define QIE_RING_DEPTH 3
+#endif
+constexpr int kRingD = QIE_RING_DEPTH;  // K slices in flight ahead of the one being multiplied
+constexpr int k4Slots = kRingD + 1;     // LDS ring slots (4: 128 KiB, 5: 160 KiB)
 // 4 = the 8-wave form (measured +3..7.5 % over the 2-stage kernel on the DiT GEMMs, bitwise equal);
 // 8 = the 4-wave form, 5 % slower: one wave per SIMD exposes each LDS-DMA piece's issue cost
-constexpr int kRingNT = 4;
+#ifndef QIE_RING_NT  // 8: the 4-wave form (see above)
+#define QIE_RING_NT 4
+#endif
+constexpr int kRingNT = QIE_RING_NT;
+
+#ifdef QIE_GEMM_STAMP
+// diagnostic build only (tools/gemm_stamp.hip): sums over waves of per-slice cycles
+__device__ unsigned long long g_gstamp[4];
+#endif
 
 __device__ __forceinline__ int swz4(int row) { return ((row >> 3) & 1) * 3; }
 
@@ -413,7 +425,7 @@ __global__ void __launch_bounds__(NT == 8 ? 256 : 512, 1)
   auto dma = [&](int kt, int p) {
     const bool isw = p >= PPW;
     const int pi = isw ? p - PPW : p;
-    char QIE_LDS* dst = smem + (kt & (k4Slots - 1)) * k4Stage + (isw ? k4Tile : 0) +
+    char QIE_LDS* dst = smem + (kt % k4Slots) * k4Stage + (isw ? k4Tile : 0) +
                         (wave + pi * NWAVE) * 1024;
     if (isw) dma_piece(wr, dst, wo[pi], kt * k4RowBytes);
     else dma_piece(xr, dst, xo[pi], kt * k4RowBytes);
@@ -425,7 +437,7 @@ __global__ void __launch_bounds__(NT == 8 ? 256 : 512, 1)
   const int a_off = (wm * 128 + fr) * k4RowBytes + cofs;
   const int w_off = k4Tile + (wn * NT * 16 + fr) * k4RowBytes + cofs;
   auto ldfrag = [&](int kt, int r) -> frag {
-    const char QIE_LDS* base = smem + (kt & (k4Slots - 1)) * k4Stage;
+    const char QIE_LDS* base = smem + (kt % k4Slots) * k4Stage;
     return *(const frag QIE_LDS*)(base + (r < 8 ? w_off + r * 16 * k4RowBytes
                                                  : a_off + (r - 8) * 16 * k4RowBytes));
   };
@@ -435,15 +447,29 @@ __global__ void __launch_bounds__(NT == 8 ? 256 : 512, 1)
 
   // slice kt: 64 MFMAs on register set CUR; interleaved reads of slice kt+1 into set CUR^1 and
   // DMA of slice kt+3 into the slot last read by slice kt-2 (consumed before this barrier)
-  auto slice = [&](auto cur_t, auto init_t, auto read_t, auto dma_t, auto wait8_t, int kt) {
+#ifdef QIE_GEMM_STAMP
+  unsigned long long st_wait = 0, st_body = 0, st_n = 0;
+#endif
+  // W: slices allowed to stay in flight when slice kt+1 must have landed
+  auto wait_bar = [&](auto n_t) {
+    constexpr int n = decltype(n_t)::value;
+    static_assert(n == 0 || n == 4 || n == 8 || n == 12 || n == 16, "vmcnt");
+    if constexpr (n == 0) asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    else if constexpr (n == 4) asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
+    else if constexpr (n == 8) asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
+    else if constexpr (n == 12) asm volatile("s_waitcnt vmcnt(12)\n\ts_barrier" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
+  };
+  auto slice = [&](auto ph_t, auto cur_t, auto init_t, auto read_t, auto dma_t, auto w_t, int kt) {
+    constexpr int PH = decltype(ph_t)::value;  // MFMA index (mod 8) after which a DMA piece goes
     constexpr int CUR = decltype(cur_t)::value;
     constexpr bool INIT = decltype(init_t)::value, READ = decltype(read_t)::value;
-    constexpr bool DMA = decltype(dma_t)::value, WAIT8 = decltype(wait8_t)::value;
-    if constexpr (READ) {  // slice kt+1 landed: one slice (2*PPW pieces) may stay in flight
-      if constexpr (!WAIT8) asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-      else if constexpr (PPW == 4) asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
-    }
+    constexpr bool DMA = decltype(dma_t)::value;
+    constexpr int W = decltype(w_t)::value;
+#ifdef QIE_GEMM_STAMP
+    const unsigned long long ta = __builtin_amdgcn_s_memtime();
+#endif
+    if constexpr (READ) wait_bar(std::integral_constant<int, W * 2 * PPW>{});  // slice kt+1 landed
 #pragma unroll
     for (int q = 0; q < 8 * NT; ++q) {
       const int i = q / NT, j = q % NT;
@@ -456,39 +482,68 @@ __global__ void __launch_bounds__(NT == 8 ? 256 : 512, 1)
         if (j == NT - 1) af[CUR ^ 1][i] = ldfrag(kt + 1, 8 + i);
       }
       if constexpr (DMA) {
-        if ((q & 7) == 3) dma(kt + 3, q >> 3);
+        if ((q & 7) == PH) dma(kt + kRingD, q >> 3);
       }
+#ifdef QIE_GEMM_STAMP
+      if (q == 0) st_wait += __builtin_amdgcn_s_memtime() - ta;
+#endif
     }
+#ifdef QIE_GEMM_STAMP
+    st_body += __builtin_amdgcn_s_memtime() - ta;
+    st_n += 1;
+#endif
   };
   using T = std::true_type;
   using F = std::false_type;
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
 
-  // prologue: slices 0..2 in flight, slice 0 landed, its fragments read
-#pragma unroll
-  for (int p = 0; p < 2 * PPW; ++p) dma(0, p);
-#pragma unroll
-  for (int p = 0; p < 2 * PPW; ++p) dma(1, p);
-#pragma unroll
-  for (int p = 0; p < 2 * PPW; ++p) dma(2, p);
-  if constexpr (PPW == 4) asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
-#pragma unroll
-  for (int r = 0; r < NT; ++r) wf[0][r] = ldfrag(0, r);
-#pragma unroll
-  for (int r = 0; r < 8; ++r) af[0][r] = ldfrag(0, 8 + r);
-  slice(I0{}, T{}, T{}, T{}, T{}, 0);  // slice 0 (nk >= 4: slice 3 exists)
-  int kt = 1;
-  for (; kt + 4 < nk; kt += 2) {  // steady state: slices kt, kt+1 both stage kt+3 / kt+4
-    slice(I1{}, F{}, T{}, T{}, T{}, kt);
-    slice(I0{}, F{}, T{}, T{}, T{}, kt + 1);
+  using W0 = std::integral_constant<int, 0>;
+  using W1 = std::integral_constant<int, 1>;
+  using W2 = std::integral_constant<int, 2>;
+  using WD = std::integral_constant<int, kRingD - 2>;  // steady state: slices kt+2 .. kt+D-1
+
+  // K loop; `ph` = MFMA index (mod 8) after which each LDS-DMA piece is issued (staggering it
+  // between the two waves of a SIMD measured -1 %, so both use the same position)
+  auto kloop = [&](auto ph) {
+    // prologue: slices 0 .. D-1 in flight, slice 0 landed, its fragments read
+  #pragma unroll
+    for (int d = 0; d < kRingD; ++d)
+  #pragma unroll
+      for (int p = 0; p < 2 * PPW; ++p) dma(d, p);
+    wait_bar(std::integral_constant<int, (kRingD - 1) * 2 * PPW>{});
+  #pragma unroll
+    for (int r = 0; r < NT; ++r) wf[0][r] = ldfrag(0, r);
+  #pragma unroll
+    for (int r = 0; r < 8; ++r) af[0][r] = ldfrag(0, 8 + r);
+    slice(ph, I0{}, T{}, T{}, T{}, WD{}, 0);  // slice 0 (host: nk >= kRingD + 2)
+    int kt = 1;
+    for (; kt + 1 + kRingD < nk; kt += 2) {  // steady state: slices kt, kt+1 stage kt+D, kt+1+D
+      slice(ph, I1{}, F{}, T{}, T{}, WD{}, kt);
+      slice(ph, I0{}, F{}, T{}, T{}, WD{}, kt + 1);
+    }
+    // tail: nk is even (host: K_bytes % 128 == 0), so exactly D or D+1 (whichever is odd) slices
+    // remain, register set 1 first (a data-dependent branch here makes hipcc spill AGPRs)
+    if constexpr (kRingD == 3) {  // slices nk-3 .. nk-1
+      slice(ph, I1{}, F{}, T{}, F{}, W1{}, kt);      // reads nk-2, everything staged
+      slice(ph, I0{}, F{}, T{}, F{}, W0{}, kt + 1);  // reads nk-1
+      slice(ph, I1{}, F{}, F{}, F{}, W0{}, kt + 2);
+    } else {  // kRingD == 4: slices nk-5 .. nk-1
+      slice(ph, I1{}, F{}, T{}, T{}, W2{}, kt);      // stages the last slice nk-1
+      slice(ph, I0{}, F{}, T{}, F{}, W2{}, kt + 1);
+      slice(ph, I1{}, F{}, T{}, F{}, W1{}, kt + 2);
+      slice(ph, I0{}, F{}, T{}, F{}, W0{}, kt + 3);
+      slice(ph, I1{}, F{}, F{}, F{}, W0{}, kt + 4);
+    }
+  };
+  kloop(std::integral_constant<int, 3>{});
+#ifdef QIE_GEMM_STAMP
+  if (lane == 0) {
+    atomicAdd(&g_gstamp[0], st_wait);
+    atomicAdd(&g_gstamp[1], st_body);
+    atomicAdd(&g_gstamp[2], st_n);
   }
-  // tail: nk is even (host: K_bytes % 128 == 0), so the loop leaves exactly slices
-  // nk-3 .. nk-1, register set 1 first (a data-dependent branch here makes hipcc spill AGPRs)
-  slice(I1{}, F{}, T{}, F{}, T{}, kt);      // reads nk-2, everything staged
-  slice(I0{}, F{}, T{}, F{}, F{}, kt + 1);  // reads nk-1: vmcnt(0)
-  slice(I1{}, F{}, F{}, F{}, F{}, kt + 2);
+#endif
   // MFMA D -> VALU read hazard for the last row of accumulators (asm is not padded by hipcc)
   if constexpr (NT == 8)
     asm volatile("s_nop 15\n\ts_nop 7"
@@ -534,7 +589,7 @@ int launch_gemm(const void* x, int64_t ldx, const void* w, int64_t ldw, int M, i
   const bool wide = N % 8 == 0 && ((uintptr_t)e.out % 16) == 0 && e.ldo % 8 == 0 &&
                     (EPI != EPI_GATE_RES || (((uintptr_t)e.gate % 16) == 0 && e.gate_bstride % 8 == 0)) &&
                     (EPI != EPI_QKV || e.head_dim % 8 == 0);
-  if (wide && M >= 256 && N >= 256 && big_tiles >= 160 && kb >= 4 * k4RowBytes) {
+  if (wide && M >= 256 && N >= 256 && big_tiles >= 160 && kb >= (kRingD + 2) * k4RowBytes) {
     gemm_ring_kernel<kRingNT, EPI, I8><<<(int)big_tiles, 2 * (256 / (kRingNT * 16)) * 64, 0, s>>>((const char*)x, ldx_b, (const char*)w, ldw_b,
                                                          M, N, kb, e);
     return qie_last_error();

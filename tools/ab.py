@@ -62,8 +62,11 @@ def main():
                                                 outs[i][1].data_ptr(), S_IMG, S_TXT, 1 / math.sqrt(128), st)
             assert rc == 0, rc
     elif what.startswith("gemm"):
-        M, N, K = {"gemm_up": (16384, 12288, 3072), "gemm_qkv": (16384, 9216, 3072),
-                   "gemm_down": (16384, 3072, 12288)}[what]
+        if what.startswith("gemm:"):  # gemm:M:N:K
+            M, N, K = (int(v) for v in what.split(":")[1:])
+        else:
+            M, N, K = {"gemm_up": (16384, 12288, 3072), "gemm_qkv": (16384, 9216, 3072),
+                       "gemm_down": (16384, 3072, 12288)}[what]
         x = torch.randn(M, K, device=dev).to(BF16)
         w = (torch.randn(N, K, device=dev) * 0.02).to(BF16)
         b = torch.zeros(N, device=dev, dtype=BF16)
