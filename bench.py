@@ -99,6 +99,8 @@ def main():
     ap.add_argument("--layers", type=int, default=60, help="debug only; the headline needs 60")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-probe", action="store_true")
+    ap.add_argument("--no-text-overlap", action="store_true",
+                    help="A/B: run the text stream on the caller's stream, not on a second HIP stream")
     ap.add_argument("--force-dist", action="store_true",
                     help="debug: run the collective path (process group, broadcast, gather, "
                          "barriers, max-reduce) even at world size 1")
@@ -123,6 +125,7 @@ def main():
     model = QwenImageTransformer2DModel(num_layers=args.layers, device=dev).random_init_(seed=0)
     if args.workload == "stream2-int8":
         model.quantize_int8()
+    model.overlap_text_stream = not args.no_text_overlap
     torch.cuda.synchronize()
     log(f"[bench] model built in {time.time() - t_build:.1f}s, "
         f"{torch.cuda.memory_allocated() / 1e9:.1f} GB")

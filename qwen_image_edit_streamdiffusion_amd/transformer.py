@@ -176,6 +176,11 @@ class QwenImageTransformer2DModel(nn.Module):
         self.probe: Optional[Dict[str, list]] = None
         self._ws: Dict[Tuple, _Workspace] = {}
         self._rope: Dict[Tuple, Tuple[torch.Tensor, ...]] = {}
+        # Text-stream work (M = B * S_txt rows: too few tiles to fill the chip) runs on a second
+        # HIP stream beside the image stream; the two only meet at the joint attention (see
+        # _block). False: everything on the caller's stream, in the same order (A/B switch).
+        self.overlap_text_stream = True
+        self._side: Optional[torch.cuda.Stream] = None
         # K % 64 requirement of the GEMM kernels for the small input projections
         if in_channels % 64 or joint_attention_dim % 64:
             raise NotImplementedError("in_channels and joint_attention_dim must be multiples of 64")
@@ -456,63 +461,109 @@ class QwenImageTransformer2DModel(nn.Module):
         ops.gemv(ws.t_hs, self.t_l2_w, self.t_l2_b, out=ws.temb)
         ops.silu(ws.temb, out=ws.stemb)
         kv_len = [S_img + l for l in txt_lens]
+        side = self._side_stream() if has_txt else None
+        if side is not None:  # the text stream starts from the prologue's x_txt and stemb
+            side.wait_stream(torch.cuda.current_stream())
         for blk in self.transformer_blocks:
-            self._block(blk, ws, B, S_img, S_txt, kv_len, icos, isin, tcos, tsin, eps)
+            self._block(blk, ws, B, S_img, S_txt, kv_len, icos, isin, tcos, tsin, eps, side)
+        if side is not None:  # the next forward's prologue rewrites x_txt
+            torch.cuda.current_stream().wait_stream(side)
         # ---- head: AdaLayerNormContinuous (scale first) + proj_out
         ops.gemv(ws.stemb, self.norm_out_w, self.norm_out_b, out=ws.emb_out)
         ops.layernorm_modulate(ws.x_img, ws.emb_out[:, D:], ws.emb_out[:, :D], S_img, out=ws.h_img,
                                eps=eps)
         ops.linear(ws.h_img, self.proj_out_w, self.proj_out_b, out=out2d)
 
-    def _block(self, blk: _Block, ws: _Workspace, B, S_img, S_txt, kv_len, icos, isin, tcos, tsin, eps):
-        D = self.config.inner_dim
+    def _side_stream(self) -> Optional[torch.cuda.Stream]:
+        if not self.overlap_text_stream:
+            return None
+        if self._side is None:
+            self._side = torch.cuda.Stream(device=self.device)
+        return self._side
+
+    def _block(self, blk: _Block, ws: _Workspace, B, S_img, S_txt, kv_len, icos, isin, tcos, tsin, eps,
+               side: Optional[torch.cuda.Stream] = None):
+        """One dual-stream block. The image and text streams are independent except at the
+        joint attention, so with ``side`` the text stream's kernels go to that HIP stream:
+          side: mod_txt, LN1, QKV (text rows of qkv), QK-norm+RoPE  -> joins main before attention
+          main: mod_img, LN1, QKV (image rows of qkv), QK-norm+RoPE, [join] attention
+          side: [fork after attention] out-proj, LN2, MLP of the text stream
+          main: out-proj, LN2, MLP of the image stream
+        Each stream writes only its own buffers (x/h/att/mlp/mod/split-K workspace, disjoint row
+        ranges of qkv); att_txt and the qkv text rows change hands at the join/fork, and the
+        next block's attention waits for the side stream's next QKV, which follows this block's
+        text out-proj in stream order."""
         R_t = B * S_txt
         has_txt = S_txt > 0
-        i8 = self.int8
-        ops.gemv(ws.stemb, blk.w_mod_img, blk.b_mod_img, out=ws.mod_img)
+        main = torch.cuda.current_stream() if side is not None else None
+        img = ("img", ws.x_img, ws.h_img, ws.att_img, ws.mlp_img, ws.mod_img, S_img, 0)
+        txt = ("txt", ws.x_txt[:R_t], ws.h_txt[:R_t], ws.att_txt[:R_t], ws.mlp_txt[:R_t], ws.mod_txt,
+               S_txt, S_img)
+        # ---- modulation, LN1 + modulate, fused QKV projection, QK RMSNorm + RoPE
         if has_txt:
-            ops.gemv(ws.stemb, blk.w_mod_txt, blk.b_mod_txt, out=ws.mod_txt)
-        mi, mt = ws.mod_img, ws.mod_txt  # chunks: shift1 scale1 gate1 shift2 scale2 gate2
-        streams = [("img", ws.x_img, ws.h_img, ws.att_img, ws.mlp_img, mi, S_img, 0)]
-        if has_txt:
-            streams.append(("txt", ws.x_txt[:R_t], ws.h_txt[:R_t], ws.att_txt[:R_t],
-                            ws.mlp_txt[:R_t], mt, S_txt, S_img))
-        # ---- LN1 + modulate, fused QKV projection into the joint buffer
-        QKV, GATE, GELU = ops.EPI_QKV, ops.EPI_GATED_RESIDUAL, ops.EPI_GELU
-        for s, x, h, att, mlp, m, rpb, seq_off in streams:
-            if i8:
-                qD, sc = self._q8(ws, s, x.shape[0], D)
-                ops.layernorm_modulate_i8(x, m[:, 0:D], m[:, D:2 * D], rpb, qD, sc, eps)
-                self._linear(ws, blk, s, "qkv", (qD, sc), QKV, ws.qkv, rpb=rpb, seq_off=seq_off)
-            else:
-                ops.layernorm_modulate(x, m[:, 0:D], m[:, D:2 * D], rpb, out=h, eps=eps)
-                self._linear(ws, blk, s, "qkv", h, QKV, ws.qkv, rpb=rpb, seq_off=seq_off)
-        # ---- QK RMSNorm + RoPE, joint attention
-        ops.qk_norm_rope(ws.qkv, 0, S_img, blk.norm_q, blk.norm_k, icos, isin, eps)
-        if has_txt:
-            ops.qk_norm_rope(ws.qkv, S_img, S_txt, blk.norm_added_q, blk.norm_added_k, tcos, tsin, eps)
+            with self._on(side):
+                self._stream_pre(blk, ws, txt, tcos, tsin, eps)
+        self._stream_pre(blk, ws, img, icos, isin, eps)
+        if side is not None:
+            main.wait_stream(side)
+        # ---- joint attention
         with self._probe("attention"):
             ops.attention(ws.qkv, kv_len, ws.att_img, ws.att_txt[:R_t] if has_txt else None, S_img, S_txt,
                           workspace=ws.attn_split)
         # ---- out-proj + gated residual, LN2 + modulate, MLP + gated residual
-        for s, x, h, att, mlp, m, rpb, seq_off in streams:
-            if i8:
-                rows, F = x.shape[0], mlp.shape[1]
-                qD, sc = self._q8(ws, s, rows, D)
-                ops.quantize_rows(att, qD, sc)
-                self._linear(ws, blk, s, "out", (qD, sc), GATE, x, gate=m[:, 2 * D:3 * D], rpb=rpb)
-                ops.layernorm_modulate_i8(x, m[:, 3 * D:4 * D], m[:, 4 * D:5 * D], rpb, qD, sc, eps)
-                with self._probe("mlp_up" if s == "img" else None):
-                    self._linear(ws, blk, s, "up", (qD, sc), GELU, mlp)
-                qF, sc = self._q8(ws, s, rows, F)
-                ops.quantize_rows(mlp, qF, sc)
-                self._linear(ws, blk, s, "down", (qF, sc), GATE, x, gate=m[:, 5 * D:6 * D], rpb=rpb)
-            else:
-                self._linear(ws, blk, s, "out", att, GATE, x, gate=m[:, 2 * D:3 * D], rpb=rpb)
-                ops.layernorm_modulate(x, m[:, 3 * D:4 * D], m[:, 4 * D:5 * D], rpb, out=h, eps=eps)
-                with self._probe("mlp_up" if s == "img" else None):
-                    self._linear(ws, blk, s, "up", h, GELU, mlp)
-                self._linear(ws, blk, s, "down", mlp, GATE, x, gate=m[:, 5 * D:6 * D], rpb=rpb)
+        if side is not None:
+            side.wait_stream(main)
+        if has_txt:
+            with self._on(side):
+                self._stream_post(blk, ws, txt, eps)
+        self._stream_post(blk, ws, img, eps)
+
+    @staticmethod
+    def _on(stream: Optional[torch.cuda.Stream]):
+        return torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()
+
+    def _stream_pre(self, blk: _Block, ws: _Workspace, st, cos, sin, eps):
+        """mod = W_mod SiLU(temb) + b; h = LN1(x)(1 + scale1) + shift1; q|k|v = h W + b into the
+        stream's rows of the joint qkv buffer; per-head RMSNorm + RoPE of q and k."""
+        s, x, h, att, mlp, m, rpb, seq_off = st
+        D = self.config.inner_dim
+        ops.gemv(ws.stemb, getattr(blk, f"w_mod_{s}"), getattr(blk, f"b_mod_{s}"), out=m)
+        # chunks of m: shift1 scale1 gate1 shift2 scale2 gate2
+        if self.int8:
+            qD, sc = self._q8(ws, s, x.shape[0], D)
+            ops.layernorm_modulate_i8(x, m[:, 0:D], m[:, D:2 * D], rpb, qD, sc, eps)
+            self._linear(ws, blk, s, "qkv", (qD, sc), ops.EPI_QKV, ws.qkv, rpb=rpb, seq_off=seq_off)
+        else:
+            ops.layernorm_modulate(x, m[:, 0:D], m[:, D:2 * D], rpb, out=h, eps=eps)
+            self._linear(ws, blk, s, "qkv", h, ops.EPI_QKV, ws.qkv, rpb=rpb, seq_off=seq_off)
+        if s == "img":
+            ops.qk_norm_rope(ws.qkv, seq_off, rpb, blk.norm_q, blk.norm_k, cos, sin, eps)
+        else:
+            ops.qk_norm_rope(ws.qkv, seq_off, rpb, blk.norm_added_q, blk.norm_added_k, cos, sin, eps)
+
+    def _stream_post(self, blk: _Block, ws: _Workspace, st, eps):
+        """x += gate1 (att W_out + b); h = LN2(x)(1 + scale2) + shift2;
+        x += gate2 (GELU_tanh(h W_up + b) W_down + b)."""
+        s, x, h, att, mlp, m, rpb, seq_off = st
+        D = self.config.inner_dim
+        GATE, GELU = ops.EPI_GATED_RESIDUAL, ops.EPI_GELU
+        if self.int8:
+            rows, F = x.shape[0], mlp.shape[1]
+            qD, sc = self._q8(ws, s, rows, D)
+            ops.quantize_rows(att, qD, sc)
+            self._linear(ws, blk, s, "out", (qD, sc), GATE, x, gate=m[:, 2 * D:3 * D], rpb=rpb)
+            ops.layernorm_modulate_i8(x, m[:, 3 * D:4 * D], m[:, 4 * D:5 * D], rpb, qD, sc, eps)
+            with self._probe("mlp_up" if s == "img" else None):
+                self._linear(ws, blk, s, "up", (qD, sc), GELU, mlp)
+            qF, sc = self._q8(ws, s, rows, F)
+            ops.quantize_rows(mlp, qF, sc)
+            self._linear(ws, blk, s, "down", (qF, sc), GATE, x, gate=m[:, 5 * D:6 * D], rpb=rpb)
+        else:
+            self._linear(ws, blk, s, "out", att, GATE, x, gate=m[:, 2 * D:3 * D], rpb=rpb)
+            ops.layernorm_modulate(x, m[:, 3 * D:4 * D], m[:, 4 * D:5 * D], rpb, out=h, eps=eps)
+            with self._probe("mlp_up" if s == "img" else None):
+                self._linear(ws, blk, s, "up", h, GELU, mlp)
+            self._linear(ws, blk, s, "down", mlp, GATE, x, gate=m[:, 5 * D:6 * D], rpb=rpb)
 
     def _linear(self, ws, blk, s: str, name: str, inp, kind: int, out, gate=None, rpb: int = 1,
                 seq_off: int = 0):
