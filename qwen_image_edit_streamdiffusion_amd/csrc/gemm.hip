@@ -4,11 +4,14 @@
 // QwenImageTransformerBlock [U] -- the 68.7 %
 // of DiT FLOPs that are linear.
 //
-// Two kernels, both gfx950-only (cdna_hip_programming.md §5):
-//   gemm_ring_kernel (big shapes: M, N >= 256, >= 160 tiles, aligned output) -- 256x256 tile,
-//     8 waves, 4-slot LDS ring of 32-wide K slices fed by buffer_load...lds three slices ahead,
-//     fragments of slice k+1 read into registers during slice k, asm MFMAs with in-place
-//     accumulators, permlane16-widened 16-byte epilogue stores. See its section below.
+// Kernels, all gfx950-only (cdna_hip_programming.md §5):
+//   gemm_pp_kernel (big shapes: M, N >= 256, >= 160 tiles, aligned output) -- 256x256 tile,
+//     8 waves in two ping-pong groups, 64-wide K tiles of whole 128-byte lines double buffered
+//     by LDS-DMA, asm MFMAs with in-place accumulators, permlane16-widened 16-byte epilogue
+//     stores. See its section below.
+//   gemm_ring_kernel (the previous big-shape kernel, build with -DQIE_GEMM_PP=0) -- the same tile
+//     with a 4-slot ring of 32-wide K slices (64-byte rows), fragments of slice k+1 read into
+//     registers during slice k.
 //   gemm_kernel (everything else: text-stream rows, small N) -- BMxBN tile, 2-stage:
 //     * both operands are K-contiguous (activation rows, nn.Linear weight rows),
 //       staged global -> LDS with 16-byte global_load_lds (LDS-DMA), one 128-byte
@@ -334,6 +337,12 @@ constexpr int k4Slots = kRingD + 1;     // LDS ring slots (4: 128 KiB, 5: 160 Ki
 #define QIE_RING_NT 4
 #endif
 constexpr int kRingNT = QIE_RING_NT;
+#ifndef QIE_GEMM_PP  // 1: gemm_pp_kernel for the big shapes (+14 % over gemm_ring in A/B); 0: gemm_ring
+#define QIE_GEMM_PP 1
+#endif
+#ifndef QIE_PP_ABL  // diagnostic ablations of gemm_pp (wrong results): 1 no DMA, 2 no LDS reads
+#define QIE_PP_ABL 0
+#endif
 
 #ifdef QIE_GEMM_STAMP
 // diagnostic build only (tools/gemm_stamp.hip): sums over waves of per-slice cycles
@@ -385,6 +394,40 @@ struct Mma4<true> {
     asm volatile("v_mfma_i32_16x16x64_i8 %0, %1, %2, 0" : "=a"(c) : "v"(a), "v"(b));
   }
 };
+
+// Epilogue of a wave's 128 x (16 NT) accumulator block at output (mrow0, ncol0) -- rows
+// mrow0 + 16i + (lane & 15), four consecutive columns per lane and tile. Every lane takes part
+// in the permlane16 swaps; rows/columns past M/N are clamped for the loads and skipped for the
+// store (N % 8 == 0, host-checked).
+template <int NT, int EPI, bool I8>
+__device__ __forceinline__ void ring_epilogue(typename MfmaOp<I8>::acc (&acc)[8][NT], const EpiArgs& e, int M,
+                                              int N, int mrow0, int ncol0, int lane) {
+  // MFMA D -> VALU read hazard for the last row of accumulators (asm is not padded by hipcc)
+  if constexpr (NT == 8)
+    asm volatile("s_nop 15\n\ts_nop 7"
+                 : "+a"(acc[7][0]), "+a"(acc[7][1]), "+a"(acc[7][2]), "+a"(acc[7][3]), "+a"(acc[7][4]),
+                   "+a"(acc[7][5]), "+a"(acc[7][NT - 2]), "+a"(acc[7][NT - 1]));
+  else
+    asm volatile("s_nop 15\n\ts_nop 7"
+                 : "+a"(acc[7][0]), "+a"(acc[7][1]), "+a"(acc[7][2]), "+a"(acc[7][3]), "+a"(acc[6][0]),
+                   "+a"(acc[6][1]), "+a"(acc[6][2]), "+a"(acc[6][NT - 1]));
+  const int g = lane >> 4, fr = lane & 15;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int m = mrow0 + i * 16 + fr;
+    const int mc = min(m, M - 1);
+#pragma unroll
+    for (int jp = 0; jp < NT / 2; ++jp) {
+      const int nb = ncol0 + jp * 32;
+      u32x2_t a = epi_pre<EPI, I8>(e, mc, min(nb + g * 4, N - 4), acc[i][2 * jp]);
+      u32x2_t b = epi_pre<EPI, I8>(e, mc, min(nb + 16 + g * 4, N - 4), acc[i][2 * jp + 1]);
+      const auto sx = __builtin_amdgcn_permlane16_swap(a.x, b.x, false, false);
+      const auto sy = __builtin_amdgcn_permlane16_swap(a.y, b.y, false, false);
+      const int n = nb + (g & 1) * 16 + (g >> 1) * 8;
+      if (m < M && n < N) epi_store8<EPI>(e, m, n, u32x4_t{sx[0], sy[0], sx[1], sy[1]});
+    }
+  }
+}
 
 // NT = 16-column MFMA tiles per wave: 8 -> 4 waves (2x2, 128x128 per wave, one wave per SIMD);
 // 4 -> 8 waves (2x4, 128x64 per wave, two per SIMD: a wave's DMA issue hides behind its partner)
@@ -544,34 +587,198 @@ __global__ void __launch_bounds__(NT == 8 ? 256 : 512, 1)
     atomicAdd(&g_gstamp[2], st_n);
   }
 #endif
-  // MFMA D -> VALU read hazard for the last row of accumulators (asm is not padded by hipcc)
-  if constexpr (NT == 8)
-    asm volatile("s_nop 15\n\ts_nop 7"
-                 : "+a"(acc[7][0]), "+a"(acc[7][1]), "+a"(acc[7][2]), "+a"(acc[7][3]), "+a"(acc[7][4]),
-                   "+a"(acc[7][5]), "+a"(acc[7][NT - 2]), "+a"(acc[7][NT - 1]));
-  else
-    asm volatile("s_nop 15\n\ts_nop 7"
-                 : "+a"(acc[7][0]), "+a"(acc[7][1]), "+a"(acc[7][2]), "+a"(acc[7][3]), "+a"(acc[6][0]),
-                   "+a"(acc[6][1]), "+a"(acc[6][2]), "+a"(acc[6][NT - 1]));
+  ring_epilogue<NT, EPI, I8>(acc, e, M, N, m0 + wm * 128, n0 + wn * NT * 16, lane);
+}
 
-  // wide epilogue; every lane takes part in the swaps, rows/columns past M/N are clamped for the
-  // loads and skipped for the store (N % 8 == 0, host-checked)
-  const int g = lane >> 4;
+// ---------------------------------------------------------------------------------------------
+// gemm_pp: the 256x256 tile with its two wave groups in ping-pong and full-line K tiles
+// (cdna_hip_programming.md §5 "256² 8-phase template" / T3-T5, MI355X_MICROARCH.md "Two waves
+// per SIMD"). Measured on the ring form: with its LDS-DMA removed the same MFMA + LDS-read loop
+// runs 1.3-1.4x faster, i.e. the 64-byte-row slices (every 1-KiB DMA piece touching 16 half-used
+// 128-byte lines) bound it. Here:
+//   * K advances in 64-wide tiles of 128-byte LDS rows (8 rows x 128 B per DMA piece: whole
+//     lines), double buffered: 2 x [X 256 rows | W 256 rows] = 128 KiB; row chunks XOR-swizzled
+//     chunk ^ ((row >> 1) & 7) (conflict-free ds_read_b128, applied on the source address);
+//   * waves 0-3 (group 0 = output rows 0-127) and 4-7 (group 1 = rows 128-255) put one wave of
+//     each group on every SIMD; group 1 runs one workgroup barrier behind group 0, so between two
+//     barriers one wave of every SIMD runs a 16-MFMA cluster while its partner reads the next
+//     cluster's fragments and issues DMA pieces (whose issue cost hides under the partner's
+//     MFMAs);
+//   * per tile and wave 4 sections (m-half, k-step): (0,0) (0,1) (1,0) (1,1); the 8 W fragments
+//     are read in sections 0-1 and kept, 4 X fragments per section;
+//   * staging: X(k+1) in sections 0-1 of tile k (its buffer's X rows were last read in section 3
+//     of tile k-1), W(k+2) in sections 2-3 of tile k (this buffer's W rows were last read in
+//     section 1 of tile k); section 3 waits vmcnt(4) = everything but W(k+2) -> tile k+1 landed;
+//   * every loader section ends with lgkmcnt(0) BEFORE its barrier, so each read has retired
+//     before the barrier behind which the next DMA into its rows is issued (WAR), and each wave's
+//     pieces of tile k+1 have landed before the barrier that precedes any read of it (RAW);
+//   * DMA pieces are inline asm: hipcc does not count them, so it adds no conservative vmcnt(0)
+//     before the LDS reads; the waits above are the only ones.
+__device__ __forceinline__ i32x4_t pp_rsrc(const char* base, int bytes) {
+  const uint64_t p = (uint64_t)base;
+  return i32x4_t{__builtin_amdgcn_readfirstlane((int)(uint32_t)p),
+                 __builtin_amdgcn_readfirstlane((int)(uint32_t)(p >> 32)),
+                 __builtin_amdgcn_readfirstlane(bytes), 0x00020000};
+}
+// one 1-KiB buffer_load_dwordx4 ... lds piece; M0 saved/set/restored inside the statement, s_nop 4
+// covers a just-readfirstlane'd SGPR operand (cdna_hip_programming.md §5.7)
+__device__ __forceinline__ void pp_dma(const i32x4_t& r, const char QIE_LDS* dst, uint32_t voff, int soff) {
+  unsigned keep;
+  const int lds = __builtin_amdgcn_readfirstlane((int)(uint32_t)(uintptr_t)dst);
+  asm volatile(
+      "s_nop 4\n\t"
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %3\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %2, %4 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(r), "s"(lds), "s"(soff)
+      : "memory");
+}
+
+constexpr int kPPTile = 256 * kRowBytes;  // one operand of one K tile, 32 KiB
+constexpr int kPPBuf = 2 * kPPTile;       // X + W, 64 KiB; two buffers
+
+template <int EPI, bool I8>
+__global__ void __launch_bounds__(512, 2)
+    gemm_pp_kernel(const char* __restrict__ X, int64_t ldx_b, const char* __restrict__ W, int64_t ldw_b,
+                   int M, int N, int K_bytes, EpiArgs e) {
+  using frag = typename MfmaOp<I8>::frag;
+  using accT = typename MfmaOp<I8>::acc;
+  constexpr int NT = 4, NWAVE = 8, PPO = 4;  // PPO: DMA pieces per wave per operand tile
+  __shared__ __attribute__((aligned(16))) char smem_raw[2 * kPPBuf];
+  char QIE_LDS* smem = (char QIE_LDS*)smem_raw;
+
+  const int tiles_m = (M + 255) >> 8, tiles_n = (N + 255) >> 8;
+  const int nwg = tiles_m * tiles_n;
+  const int wgid = xcd_remap(blockIdx.x, nwg);
+  constexpr int GROUP = 8;
+  const int per_group = GROUP * tiles_n;
+  const int first_m = (wgid / per_group) * GROUP;
+  const int gsz = min(tiles_m - first_m, GROUP);
+  const int tm = first_m + (wgid % per_group) % gsz;
+  const int tn = (wgid % per_group) / gsz;
+  const int m0 = tm * 256, n0 = tn * 256;
+
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int wm = wave >> 2, wn = wave & 3;  // wm is also the ping-pong group
+  const int m_valid = M - m0, n_valid = N - n0;
+  const int nk = K_bytes / kRowBytes;  // host guarantees nk >= 3
+
+  const i32x4_t xr = pp_rsrc(X + (int64_t)m0 * ldx_b, (int)(min(m_valid, 256) * ldx_b));
+  const i32x4_t wr = pp_rsrc(W + (int64_t)n0 * ldw_b, (int)(min(n_valid, 256) * ldw_b));
+  // piece i of an operand tile: rows 8 (wave + 8 i) .. +7, lane -> row + (lane >> 3), swizzled chunk
+  uint32_t xo[PPO], wo[PPO];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int m = m0 + wm * 128 + i * 16 + fr;
-    const int mc = min(m, M - 1);
-#pragma unroll
-    for (int jp = 0; jp < NT / 2; ++jp) {
-      const int nb = n0 + wn * NT * 16 + jp * 32;
-      u32x2_t a = epi_pre<EPI, I8>(e, mc, min(nb + g * 4, N - 4), acc[i][2 * jp]);
-      u32x2_t b = epi_pre<EPI, I8>(e, mc, min(nb + 16 + g * 4, N - 4), acc[i][2 * jp + 1]);
-      const auto sx = __builtin_amdgcn_permlane16_swap(a.x, b.x, false, false);
-      const auto sy = __builtin_amdgcn_permlane16_swap(a.y, b.y, false, false);
-      const int n = nb + (g & 1) * 16 + (g >> 1) * 8;
-      if (m < M && n < N) epi_store8<EPI>(e, m, n, u32x4_t{sx[0], sy[0], sx[1], sy[1]});
-    }
+  for (int i = 0; i < PPO; ++i) {
+    const int r = (wave + i * NWAVE) * 8 + (lane >> 3);
+    const int c = swz_chunk(r, lane & 7);
+    xo[i] = (uint32_t)(min(r, m_valid - 1) * ldx_b) + (c << 4);
+    wo[i] = (uint32_t)(min(r, n_valid - 1) * ldw_b) + (c << 4);
   }
+  auto dmaX = [&](int kt, int i) {
+    pp_dma(xr, smem + (kt & 1) * kPPBuf + (wave + i * NWAVE) * 1024, xo[i], kt * kRowBytes);
+  };
+  auto dmaW = [&](int kt, int i) {
+    pp_dma(wr, smem + (kt & 1) * kPPBuf + kPPTile + (wave + i * NWAVE) * 1024, wo[i], kt * kRowBytes);
+  };
+
+  // fragment of k-step ks: lane reads row (lane & 15) of its 16-row block, chunk 4 ks + (lane >> 4)
+  const int fr = lane & 15;
+  const int a_row = wm * 128 + fr, w_row = wn * NT * 16 + fr;
+  const int sw = (fr >> 1) & 7;  // swz_chunk term; (row + 16 i) >> 1 & 7 == row >> 1 & 7
+  auto ldX = [&](int kt, int i, int ks) -> frag {
+    return *(const frag QIE_LDS*)(smem + (kt & 1) * kPPBuf + (a_row + 16 * i) * kRowBytes +
+                                  (((4 * ks + (lane >> 4)) ^ sw) << 4));
+  };
+  auto ldW = [&](int kt, int j, int ks) -> frag {
+    return *(const frag QIE_LDS*)(smem + (kt & 1) * kPPBuf + kPPTile + (w_row + 16 * j) * kRowBytes +
+                                  (((4 * ks + (lane >> 4)) ^ sw) << 4));
+  };
+
+  accT acc[8][NT];
+  frag wf[2][NT], af[4];
+
+  // loader-section end: lgkmcnt(0) and, when n >= 0, vmcnt(n), then the barrier
+  auto ld_end = [&](auto n_t) {
+    constexpr int n = decltype(n_t)::value;
+    static_assert(n == -1 || n == 0 || n == 4 || n == 8, "vmcnt");
+    if constexpr (n == -1) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else if constexpr (n == 0) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else if constexpr (n == 4) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  };
+  // section (MH, KS) of tile kt. DX: stage X(kt+1) pieces 2 KS, 2 KS + 1 (sections MH = 0);
+  // DW: stage W(kt+2) pieces 2 KS, 2 KS + 1 (sections MH = 1); VM: vmcnt of section (1, 1)
+  auto section = [&](auto mh_t, auto ks_t, auto init_t, auto dx_t, auto dw_t, auto vm_t, int kt) {
+    constexpr int MH = decltype(mh_t)::value, KS = decltype(ks_t)::value;
+    constexpr bool INIT = decltype(init_t)::value && KS == 0;
+    constexpr bool DX = decltype(dx_t)::value, DW = decltype(dw_t)::value;
+    if constexpr (!(QIE_PP_ABL & 2) || decltype(init_t)::value) {
+      if constexpr (MH == 0) {
+#pragma unroll
+        for (int j = 0; j < NT; ++j) wf[KS][j] = ldW(kt, j, KS);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = ldX(kt, 4 * MH + i, KS);
+    }
+    if constexpr (!(QIE_PP_ABL & 1)) {
+      if constexpr (DX) {
+        dmaX(kt + 1, 2 * KS);
+        dmaX(kt + 1, 2 * KS + 1);
+      }
+      if constexpr (DW) {
+        dmaW(kt + 2, 2 * KS);
+        dmaW(kt + 2, 2 * KS + 1);
+      }
+    }
+    if constexpr (MH == 1 && KS == 1) ld_end(vm_t);
+    else ld_end(std::integral_constant<int, -1>{});
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        if constexpr (INIT) Mma4<I8>::init(acc[4 * MH + i][j], wf[KS][j], af[i]);
+        else Mma4<I8>::acc(acc[4 * MH + i][j], wf[KS][j], af[i]);
+      }
+    __builtin_amdgcn_s_setprio(0);
+    asm volatile("s_barrier" ::: "memory");
+  };
+  using T = std::true_type;
+  using F = std::false_type;
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using VNone = std::integral_constant<int, -1>;
+  using V0 = std::integral_constant<int, 0>;
+  using V4 = std::integral_constant<int, 4>;
+  // tile kt: X(kt+1) if DX, W(kt+2) if DW; section (1,1) waits for tile kt+1
+  auto tile = [&](auto init_t, auto dx_t, auto dw_t, auto vm_t, int kt) {
+    section(I0{}, I0{}, init_t, dx_t, F{}, VNone{}, kt);
+    section(I0{}, I1{}, init_t, dx_t, F{}, VNone{}, kt);
+    section(I1{}, I0{}, init_t, F{}, dw_t, VNone{}, kt);
+    section(I1{}, I1{}, init_t, F{}, dw_t, vm_t, kt);
+  };
+
+  // prologue: W(0), X(0), W(1); wait for the first two; group 1 one barrier behind
+#pragma unroll
+  for (int i = 0; i < PPO; ++i) dmaW(0, i);
+#pragma unroll
+  for (int i = 0; i < PPO; ++i) dmaX(0, i);
+#pragma unroll
+  for (int i = 0; i < PPO; ++i) dmaW(1, i);
+  ld_end(V4{});
+  if (wm == 1) asm volatile("s_barrier" ::: "memory");
+
+  tile(T{}, T{}, T{}, V4{}, 0);
+  int kt = 1;
+  for (; kt < nk - 2; ++kt) tile(F{}, T{}, T{}, V4{}, kt);
+  tile(F{}, T{}, F{}, V0{}, kt);         // nk-2: stages X(nk-1), waits for it
+  tile(F{}, F{}, F{}, VNone{}, kt + 1);  // nk-1
+  if (wm == 0) asm volatile("s_barrier" ::: "memory");  // every wave passes the same barrier count
+
+  ring_epilogue<NT, EPI, I8>(acc, e, M, N, m0 + wm * 128, n0 + wn * NT * 16, lane);
 }
 
 template <int EPI, bool I8>
@@ -590,8 +797,12 @@ int launch_gemm(const void* x, int64_t ldx, const void* w, int64_t ldw, int M, i
                     (EPI != EPI_GATE_RES || (((uintptr_t)e.gate % 16) == 0 && e.gate_bstride % 8 == 0)) &&
                     (EPI != EPI_QKV || e.head_dim % 8 == 0);
   if (wide && M >= 256 && N >= 256 && big_tiles >= 160 && kb >= (kRingD + 2) * k4RowBytes) {
-    gemm_ring_kernel<kRingNT, EPI, I8><<<(int)big_tiles, 2 * (256 / (kRingNT * 16)) * 64, 0, s>>>((const char*)x, ldx_b, (const char*)w, ldw_b,
-                                                         M, N, kb, e);
+    if constexpr (QIE_GEMM_PP)  // (kb % 128 == 0 and kb >= 320 hold, so nk >= 3)
+      gemm_pp_kernel<EPI, I8><<<(int)big_tiles, 512, 0, s>>>((const char*)x, ldx_b, (const char*)w, ldw_b, M,
+                                                            N, kb, e);
+    else
+      gemm_ring_kernel<kRingNT, EPI, I8><<<(int)big_tiles, 2 * (256 / (kRingNT * 16)) * 64, 0, s>>>(
+          (const char*)x, ldx_b, (const char*)w, ldw_b, M, N, kb, e);
     return qie_last_error();
   }
   if (M >= 256 && N >= 256 && big_tiles >= 160) {

@@ -8,6 +8,7 @@ All libraries are loaded side by side with ctypes; launches alternate A, B, C, A
 on the same random inputs (headline shapes: attention B=2, S=8408; the three DiT GEMMs)."""
 import ctypes
 import math
+import os
 import statistics
 import sys
 
@@ -70,6 +71,9 @@ def main():
         x = torch.randn(M, K, device=dev).to(BF16)
         w = (torch.randn(N, K, device=dev) * 0.02).to(BF16)
         b = torch.zeros(N, device=dev, dtype=BF16)
+        if os.environ.get("AB_ZERO"):  # zero-filled operands: the DVFS ceiling (rule 25)
+            x.zero_()
+            w.zero_()
         outs = [torch.empty(M, N, dtype=BF16, device=dev) for _ in libs]
         flops = 2.0 * M * N * K
 

@@ -1,0 +1,16 @@
+#!/bin/bash
+# Build a variant of libqie.so with extra compile flags, for same-process A/B (tools/ab.py).
+#   bash tools/build_variant.sh <name> [-DFLAG=V ...]   ->  tools/ab_build/<name>.so
+set -e
+cd "$(dirname "$0")/.."
+NAME=$1; shift
+OUT=tools/ab_build/$NAME
+mkdir -p $OUT
+for f in qwen_image_edit_streamdiffusion_amd/csrc/*.hip; do
+  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-function "$@" \
+    -c $f -o $OUT/$(basename $f .hip).o &
+done
+wait
+/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o tools/ab_build/$NAME.so $OUT/*.o
+rm -rf $OUT
+echo tools/ab_build/$NAME.so
