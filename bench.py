@@ -99,6 +99,8 @@ def main():
     ap.add_argument("--layers", type=int, default=60, help="debug only; the headline needs 60")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-probe", action="store_true")
+    ap.add_argument("--no-qk-fusion", action="store_true",
+                    help="A/B: image QKV GEMM and QK RMSNorm+RoPE as two launches")
     ap.add_argument("--no-text-overlap", action="store_true",
                     help="A/B: run the text stream on the caller's stream, not on a second HIP stream")
     ap.add_argument("--force-dist", action="store_true",
@@ -126,6 +128,7 @@ def main():
     if args.workload == "stream2-int8":
         model.quantize_int8()
     model.overlap_text_stream = not args.no_text_overlap
+    model.fuse_qk_norm_rope = not args.no_qk_fusion
     torch.cuda.synchronize()
     log(f"[bench] model built in {time.time() - t_build:.1f}s, "
         f"{torch.cuda.memory_allocated() / 1e9:.1f} GB")

@@ -104,6 +104,18 @@ int qie_qk_norm_rope_bf16(void* qkv, int batch, int heads, int head_dim, int s_p
                           int seg_len, const void* wq, const void* wk, const float* cos_tab,
                           const float* sin_tab, float eps, qie_stream_t stream);
 
+/* K1 + K7 fused -- the q|k|v projection of one stream (as qie_linear_qkv_bf16) followed by
+ * attn.norm_q/norm_k (norm_added_q/k) RMSNorm(head_dim) and apply_rotary_emb_qwen [U] on its q
+ * and k rows, with the rounding points of qie_qk_norm_rope_bf16. head_dim == 128; cos_tab /
+ * sin_tab: fp32 [rows_per_batch][64] for this stream's segment. Big shapes run as ONE GEMM
+ * whose epilogue normalises and rotates each head (the two halves of a head meet through LDS);
+ * other shapes run the GEMM and then qie_qk_norm_rope_bf16. */
+int qie_linear_qkv_norm_rope_bf16(const void* x, int64_t ldx, const void* w, const void* bias, void* qkv,
+                                  int M, int K, int rows_per_batch, int seq_offset, int batch, int heads,
+                                  int head_dim, int s_pad, const void* wq, const void* wk,
+                                  const float* cos_tab, const float* sin_tab, float eps,
+                                  qie_stream_t stream);
+
 /* ------------------------------------------------------------------ attention */
 
 /* K8 -- joint non-causal SDPA of QwenDoubleStreamAttnProcessor2_0 [U] over the
@@ -195,6 +207,13 @@ int qie_linear_qkv_i8(const void* xq, int64_t ldx, const float* sx, const void* 
                       const float* sw, const void* bias, void* qkv, int M, int K,
                       int rows_per_batch, int seq_offset, int batch, int heads, int head_dim,
                       int s_pad, qie_stream_t stream);
+
+/* qie_linear_qkv_norm_rope_bf16 on the int8 linear (dequant epilogue as qie_linear_qkv_i8). */
+int qie_linear_qkv_norm_rope_i8(const void* xq, int64_t ldx, const float* sx, const void* wq,
+                                const float* sw, const void* bias, void* qkv, int M, int K,
+                                int rows_per_batch, int seq_offset, int batch, int heads, int head_dim,
+                                int s_pad, const void* nq, const void* nk, const float* cos_tab,
+                                const float* sin_tab, float eps, qie_stream_t stream);
 
 /* ---- split-K linears for short-M shapes (the text stream, M = B * S_txt) ---------------------
  * Replaces the same diffusers linears as the entry points above (text-stream add_q/k/v_proj,

@@ -38,6 +38,7 @@ SIGNATURES = {
     "qie_linear_bf16": [P, L, P, P, P, L, I, I, I, I, P],
     "qie_linear_gated_residual_bf16": [P, L, P, P, P, L, I, P, L, I, I, I, P],
     "qie_linear_qkv_bf16": [P, L, P, P, P, I, I, I, I, I, I, I, I, P],
+    "qie_linear_qkv_norm_rope_bf16": [P, L, P, P, P, I, I, I, I, I, I, I, I, P, P, P, P, F, P],
     "qie_gemv_bf16": [P, L, P, P, P, L, I, I, I, P],
     "qie_layernorm_modulate_bf16": [P, L, P, P, L, I, P, L, I, I, F, P],
     "qie_rmsnorm_bf16": [P, P, P, I, I, F, P],
@@ -57,6 +58,7 @@ SIGNATURES = {
     "qie_linear_i8": [P, L, P, P, P, P, P, L, I, I, I, I, P],
     "qie_linear_gated_residual_i8": [P, L, P, P, P, P, P, L, I, P, L, I, I, I, P],
     "qie_linear_qkv_i8": [P, L, P, P, P, P, P, I, I, I, I, I, I, I, I, P],
+    "qie_linear_qkv_norm_rope_i8": [P, L, P, P, P, P, P, I, I, I, I, I, I, I, I, P, P, P, P, F, P],
     "qie_linear_splitk_bf16": [P, L, P, P, P, I, I, I, I, P, L, P],
     "qie_linear_splitk_i8": [P, L, P, P, P, P, P, I, I, I, I, P, L, P],
 }

@@ -30,7 +30,8 @@ namespace {
 
 constexpr int kRowBytes = 128;  // one LDS tile row = 64 bf16 or 128 int8 of K
 
-enum Epi { EPI_BIAS = 0, EPI_GELU = 1, EPI_GATE_RES = 2, EPI_QKV = 3, EPI_PARTIAL = 4 };
+// EPI_QKV_NR: EPI_QKV + the per-head RMSNorm of q and k and their RoPE (gemm_pp only)
+enum Epi { EPI_BIAS = 0, EPI_GELU = 1, EPI_GATE_RES = 2, EPI_QKV = 3, EPI_PARTIAL = 4, EPI_QKV_NR = 5 };
 
 struct EpiArgs {
   void* out;          // y / resid / qkv base
@@ -46,6 +47,12 @@ struct EpiArgs {
   const float* sw;
   // split-K partial sums (EPI_PARTIAL): [splits][M][N] fp32 (bf16) or int32 (int8)
   void* ws;
+  // EPI_QKV_NR: RMSNorm weights of q / k (head_dim), RoPE cos / sin [rows_per_batch][head_dim/2]
+  const bf16_t* nq;
+  const bf16_t* nk;
+  const float* rcos;
+  const float* rsin;
+  float eps;
 };
 
 __device__ __forceinline__ int swz_chunk(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
@@ -397,11 +404,16 @@ struct Mma4<true> {
 
 // Epilogue of a wave's 128 x (16 NT) accumulator block at output (mrow0, ncol0) -- rows
 // mrow0 + 16i + (lane & 15), four consecutive columns per lane and tile. Every lane takes part
-// in the permlane16 swaps; rows/columns past M/N are clamped for the loads and skipped for the
-// store (N % 8 == 0, host-checked).
+// in the permlane16 swaps, after which a lane holds 8 consecutive columns of one row; rows/columns
+// past M/N are clamped for the loads and skipped for the store (N % 8 == 0, host-checked).
+// EPI_QKV / EPI_QKV_NR with head_dim == 128 (host-checked for NR): the wave's 64 columns lie in
+// one head of one of q/k/v, so the scatter address is computed once per wave and row. EPI_QKV_NR
+// also applies the per-head RMSNorm (fp32 sum of squares over the head's 128 columns: the wave's
+// 64 + its partner wave's 64, exchanged through `smem`) and the RoPE rotation of q and k, with
+// the rounding points of qie_qk_norm_rope_bf16; it needs every wave of the workgroup here.
 template <int NT, int EPI, bool I8>
 __device__ __forceinline__ void ring_epilogue(typename MfmaOp<I8>::acc (&acc)[8][NT], const EpiArgs& e, int M,
-                                              int N, int mrow0, int ncol0, int lane) {
+                                              int N, int mrow0, int ncol0, int lane, char QIE_LDS* smem) {
   // MFMA D -> VALU read hazard for the last row of accumulators (asm is not padded by hipcc)
   if constexpr (NT == 8)
     asm volatile("s_nop 15\n\ts_nop 7"
@@ -412,19 +424,119 @@ __device__ __forceinline__ void ring_epilogue(typename MfmaOp<I8>::acc (&acc)[8]
                  : "+a"(acc[7][0]), "+a"(acc[7][1]), "+a"(acc[7][2]), "+a"(acc[7][3]), "+a"(acc[6][0]),
                    "+a"(acc[6][1]), "+a"(acc[6][2]), "+a"(acc[6][NT - 1]));
   const int g = lane >> 4, fr = lane & 15;
+  constexpr bool QKV = EPI == EPI_QKV || EPI == EPI_QKV_NR;
+  if constexpr (QKV && NT == 4) {
+    if (EPI == EPI_QKV_NR || e.head_dim == 128) {
+      const int hd = e.heads * 128;
+      const int which = ncol0 / hd;
+      const int h = (ncol0 - which * hd) >> 7;
+      const int dbase = ncol0 & 127;               // 0 or 64
+      const int dl = (g & 1) * 16 + (g >> 1) * 8;  // the lane's column offset inside a 32-col pair
+      // the lane's 8 consecutive bf16 of row i, column pair jp (bias added, rounded)
+      auto cols8 = [&](int i, int jp) -> u32x4_t {
+        const int mc = min(mrow0 + i * 16 + fr, M - 1);
+        const int nb = ncol0 + jp * 32;
+        u32x2_t a = epi_pre<EPI, I8>(e, mc, nb + g * 4, acc[i][2 * jp]);
+        u32x2_t b = epi_pre<EPI, I8>(e, mc, nb + 16 + g * 4, acc[i][2 * jp + 1]);
+        const auto sx = __builtin_amdgcn_permlane16_swap(a.x, b.x, false, false);
+        const auto sy = __builtin_amdgcn_permlane16_swap(a.y, b.y, false, false);
+        return u32x4_t{sx[0], sy[0], sx[1], sy[1]};
+      };
+      auto row_ptr = [&](int m) -> bf16_t* {
+        const int b = m / e.rows_per_batch;
+        const int s = e.seq_offset + (m - b * e.rows_per_batch);
+        return (bf16_t*)e.out + ((((int64_t)which * e.batch + b) * e.heads + h) * e.s_pad + s) * 128 + dbase + dl;
+      };
+      bool done = false;
+      if constexpr (EPI == EPI_QKV_NR) {
+        if (which < 2) {
+          // pass 1: sum of squares of the rounded values over the wave's 64 columns of each row,
+          // plus the partner wave's 64 (the other half of the head) through LDS
+          float ss[8];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int m = mrow0 + i * 16 + fr;
-    const int mc = min(m, M - 1);
+          for (int i = 0; i < 8; ++i) {
+            float t = 0.f;
 #pragma unroll
-    for (int jp = 0; jp < NT / 2; ++jp) {
-      const int nb = ncol0 + jp * 32;
-      u32x2_t a = epi_pre<EPI, I8>(e, mc, min(nb + g * 4, N - 4), acc[i][2 * jp]);
-      u32x2_t b = epi_pre<EPI, I8>(e, mc, min(nb + 16 + g * 4, N - 4), acc[i][2 * jp + 1]);
-      const auto sx = __builtin_amdgcn_permlane16_swap(a.x, b.x, false, false);
-      const auto sy = __builtin_amdgcn_permlane16_swap(a.y, b.y, false, false);
-      const int n = nb + (g & 1) * 16 + (g >> 1) * 8;
-      if (m < M && n < N) epi_store8<EPI>(e, m, n, u32x4_t{sx[0], sy[0], sx[1], sy[1]});
+            for (int jp = 0; jp < 2; ++jp) {
+              const u32x4_t v = cols8(i, jp);
+              const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+              for (int k = 0; k < 4; ++k) {
+                const float lo = lo_f(w4[k]), hi = hi_f(w4[k]);
+                t += lo * lo + hi * hi;
+              }
+            }
+            t += __shfl_xor(t, 16, 64);
+            t += __shfl_xor(t, 32, 64);
+            ss[i] = t;
+          }
+          const int wave = threadIdx.x >> 6;
+          float QIE_LDS* red = (float QIE_LDS*)smem;
+          if (g == 0) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) red[wave * 128 + i * 16 + fr] = ss[i];
+          }
+          __syncthreads();
+#pragma unroll
+          for (int i = 0; i < 8; ++i) ss[i] = rsqrtf((ss[i] + red[(wave ^ 1) * 128 + i * 16 + fr]) * (1.0f / 128.0f) + e.eps);
+          const bf16_t* nw = which == 0 ? e.nq : e.nk;
+          // pass 2: recompute the rounded values, RMSNorm (two bf16 roundings) and rotate
+#pragma unroll
+          for (int jp = 0; jp < 2; ++jp) {
+            const int d0 = dbase + jp * 32 + dl;
+            const u32x4_t ww = *(const u32x4_t*)(nw + d0);
+            const uint32_t wv[4] = {ww.x, ww.y, ww.z, ww.w};
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+              const int m = mrow0 + i * 16 + fr;
+              const int sl = min(m, M - 1) % e.rows_per_batch;  // row of the segment's RoPE table
+              const f32x4_t cs = *(const f32x4_t*)(e.rcos + (int64_t)sl * 64 + (d0 >> 1));
+              const f32x4_t sn = *(const f32x4_t*)(e.rsin + (int64_t)sl * 64 + (d0 >> 1));
+              const u32x4_t v = cols8(i, jp);
+              const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+              uint32_t o[4];
+#pragma unroll
+              for (int k = 0; k < 4; ++k) {
+                const float x0 = rbf(rbf(lo_f(w4[k]) * ss[i]) * lo_f(wv[k]));
+                const float x1 = rbf(rbf(hi_f(w4[k]) * ss[i]) * hi_f(wv[k]));
+                o[k] = pack2(x0 * cs[k] - x1 * sn[k], x0 * sn[k] + x1 * cs[k]);
+              }
+              if (m < M) *(u32x4_t*)(row_ptr(m) + jp * 32) = u32x4_t{o[0], o[1], o[2], o[3]};
+            }
+          }
+          done = true;
+        }
+      }
+      if (!done) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int m = mrow0 + i * 16 + fr;
+          const u32x4_t v0 = cols8(i, 0), v1 = cols8(i, 1);
+          if (m < M) {
+            bf16_t* row = row_ptr(m);
+            *(u32x4_t*)row = v0;
+            *(u32x4_t*)(row + 32) = v1;
+          }
+        }
+      }
+      return;
+    }
+  }
+  if constexpr (EPI != EPI_QKV_NR) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int m = mrow0 + i * 16 + fr;
+      const int mc = min(m, M - 1);
+#pragma unroll
+      for (int jp = 0; jp < NT / 2; ++jp) {
+        const int nb = ncol0 + jp * 32;
+        u32x2_t a = epi_pre<EPI, I8>(e, mc, min(nb + g * 4, N - 4), acc[i][2 * jp]);
+        u32x2_t b = epi_pre<EPI, I8>(e, mc, min(nb + 16 + g * 4, N - 4), acc[i][2 * jp + 1]);
+        const auto sx = __builtin_amdgcn_permlane16_swap(a.x, b.x, false, false);
+        const auto sy = __builtin_amdgcn_permlane16_swap(a.y, b.y, false, false);
+        const int n = nb + (g & 1) * 16 + (g >> 1) * 8;
+        if (m < M && n < N) epi_store8<EPI>(e, m, n, u32x4_t{sx[0], sy[0], sx[1], sy[1]});
+      }
     }
   }
 }
@@ -587,7 +699,7 @@ __global__ void __launch_bounds__(NT == 8 ? 256 : 512, 1)
     atomicAdd(&g_gstamp[2], st_n);
   }
 #endif
-  ring_epilogue<NT, EPI, I8>(acc, e, M, N, m0 + wm * 128, n0 + wn * NT * 16, lane);
+  ring_epilogue<NT, EPI, I8>(acc, e, M, N, m0 + wm * 128, n0 + wn * NT * 16, lane, smem);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -778,7 +890,7 @@ __global__ void __launch_bounds__(512, 2)
   tile(F{}, F{}, F{}, VNone{}, kt + 1);  // nk-1
   if (wm == 0) asm volatile("s_barrier" ::: "memory");  // every wave passes the same barrier count
 
-  ring_epilogue<NT, EPI, I8>(acc, e, M, N, m0 + wm * 128, n0 + wn * NT * 16, lane);
+  ring_epilogue<NT, EPI, I8>(acc, e, M, N, m0 + wm * 128, n0 + wn * NT * 16, lane, smem);
 }
 
 template <int EPI, bool I8>
@@ -867,6 +979,39 @@ int launch_splitk(const void* x, int64_t ldx, const void* w, int M, int N, int K
     default: splitk_reduce_kernel<EPI_QKV, I8><<<nb, 256, 0, s>>>(e, M, N, splits); break;
   }
   return qie_last_error();
+}
+
+// QKV projection + QK RMSNorm + RoPE of one stream's rows: ONE gemm_pp launch (EPI_QKV_NR) when the
+// shape takes the big-tile path, otherwise the QKV GEMM followed by qie_qk_norm_rope_bf16 on the
+// same rows (the same arithmetic in two launches).
+template <bool I8>
+int launch_qkv_norm_rope(const void* x, int64_t ldx, const void* w, int M, int K, EpiArgs e,
+                         const void* nq, const void* nk, const float* cos_tab, const float* sin_tab,
+                         float eps, hipStream_t s) {
+  QIE_CHECK_ARG(nq && nk && cos_tab && sin_tab && e.head_dim == 128);
+  const int N = 3 * e.heads * e.head_dim;
+  const int eb = I8 ? 1 : 2;
+  const int64_t big_tiles = (int64_t)((M + 255) / 256) * ((N + 255) / 256);
+  const bool fused = QIE_GEMM_PP && e.heads % 2 == 0 && M >= 256 && big_tiles >= 160 &&
+                     (int64_t)K * eb >= 3 * kRowBytes && ((int64_t)K * eb) % kRowBytes == 0 &&
+                     ((ldx * eb) % 16) == 0 && ((uintptr_t)x % 16) == 0 && ((uintptr_t)w % 16) == 0 &&
+                     ((uintptr_t)e.out % 16) == 0 && ((uintptr_t)nq % 16) == 0 && ((uintptr_t)nk % 16) == 0 &&
+                     ((uintptr_t)cos_tab % 16) == 0 && ((uintptr_t)sin_tab % 16) == 0;
+  if (fused) {
+    QIE_CHECK_ARG(x && w && e.out && e.bias);
+    e.nq = (const bf16_t*)nq;
+    e.nk = (const bf16_t*)nk;
+    e.rcos = cos_tab;
+    e.rsin = sin_tab;
+    e.eps = eps;
+    gemm_pp_kernel<EPI_QKV_NR, I8><<<(int)big_tiles, 512, 0, s>>>((const char*)x, ldx * eb, (const char*)w,
+                                                                 (int64_t)K * eb, M, N, K * eb, e);
+    return qie_last_error();
+  }
+  const int rc = launch_gemm<EPI_QKV, I8>(x, ldx, w, K, M, N, K, e, s);
+  if (rc) return rc;
+  return qie_qk_norm_rope_bf16(e.out, e.batch, e.heads, e.head_dim, e.s_pad, e.seq_offset, e.rows_per_batch,
+                               nq, nk, cos_tab, sin_tab, eps, s);
 }
 
 EpiArgs make_epi(void* out, int64_t ldo, const void* bias) {
@@ -969,6 +1114,32 @@ extern "C" int qie_linear_qkv_i8(const void* xq, int64_t ldx, const float* sx, c
   if (rc) return rc;
   return launch_gemm<EPI_QKV, true>(xq, ldx, wq, K, M, 3 * heads * head_dim, K, e,
                                     (hipStream_t)stream);
+}
+
+extern "C" int qie_linear_qkv_norm_rope_bf16(const void* x, int64_t ldx, const void* w, const void* bias,
+                                             void* qkv, int M, int K, int rows_per_batch, int seq_offset,
+                                             int batch, int heads, int head_dim, int s_pad, const void* wq,
+                                             const void* wk, const float* cos_tab, const float* sin_tab,
+                                             float eps, qie_stream_t stream) {
+  EpiArgs e = make_epi(qkv, 0, bias);
+  int rc = qkv_args(e, M, rows_per_batch, seq_offset, batch, heads, head_dim, s_pad);
+  if (rc) return rc;
+  return launch_qkv_norm_rope<false>(x, ldx, w, M, K, e, wq, wk, cos_tab, sin_tab, eps, (hipStream_t)stream);
+}
+
+extern "C" int qie_linear_qkv_norm_rope_i8(const void* xq, int64_t ldx, const float* sx, const void* wq,
+                                           const float* sw, const void* bias, void* qkv, int M, int K,
+                                           int rows_per_batch, int seq_offset, int batch, int heads,
+                                           int head_dim, int s_pad, const void* nq, const void* nk,
+                                           const float* cos_tab, const float* sin_tab, float eps,
+                                           qie_stream_t stream) {
+  QIE_CHECK_ARG(sx && sw);
+  EpiArgs e = make_epi(qkv, 0, bias);
+  e.sx = sx;
+  e.sw = sw;
+  int rc = qkv_args(e, M, rows_per_batch, seq_offset, batch, heads, head_dim, s_pad);
+  if (rc) return rc;
+  return launch_qkv_norm_rope<true>(xq, ldx, wq, M, K, e, nq, nk, cos_tab, sin_tab, eps, (hipStream_t)stream);
 }
 
 // ---------------------------------------------------------------------------- split-K C ABI

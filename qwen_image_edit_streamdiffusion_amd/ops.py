@@ -106,6 +106,32 @@ def linear_qkv(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, qkv: torch.Ten
               seq_offset, B, H, Dh, S_pad, _stream())
 
 
+def _rope_chk(qkv, rows_per_batch, wq, wk, cos_tab, sin_tab):
+    _dev(wq, wk, cos_tab, sin_tab)
+    Dh = qkv.shape[-1]
+    _chk(Dh == 128 and wq.numel() == Dh and wk.numel() == Dh and wq.is_contiguous() and wk.is_contiguous(),
+         "norm weights [128]")
+    _chk(cos_tab.dtype == torch.float32 and cos_tab.is_contiguous() and sin_tab.is_contiguous() and
+         cos_tab.shape == sin_tab.shape and cos_tab.shape[0] >= rows_per_batch and cos_tab.shape[1] == 64,
+         "rope table [rows_per_batch, 64] fp32")
+
+
+def linear_qkv_norm_rope(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, qkv: torch.Tensor,
+                         rows_per_batch: int, seq_offset: int, wq: torch.Tensor, wk: torch.Tensor,
+                         cos_tab: torch.Tensor, sin_tab: torch.Tensor, eps: float = 1e-6) -> None:
+    """linear_qkv followed by qk_norm_rope on the same rows, fused into the GEMM epilogue
+    where the shape allows (qie_linear_qkv_norm_rope_bf16)."""
+    _dev(x, w, b, qkv)
+    M, K = x.shape
+    _, B, H, S_pad, Dh = qkv.shape
+    _chk(qkv.is_contiguous() and w.shape == (3 * H * Dh, K) and b.numel() == 3 * H * Dh, "qkv shapes")
+    _chk(M == B * rows_per_batch and seq_offset + rows_per_batch <= S_pad, "qkv rows")
+    _chk(K % 64 == 0 and _is2d_rowmajor(x), "qkv K")
+    _rope_chk(qkv, rows_per_batch, wq, wk, cos_tab, sin_tab)
+    _lib.call("qie_linear_qkv_norm_rope_bf16", _p(x), x.stride(0), _p(w), _p(b), _p(qkv), M, K, rows_per_batch,
+              seq_offset, B, H, Dh, S_pad, _p(wq), _p(wk), _p(cos_tab), _p(sin_tab), eps, _stream())
+
+
 # ---------------------------------------------------------------------------- norms
 def layernorm_modulate(x: torch.Tensor, shift: torch.Tensor, scale: torch.Tensor, rows_per_batch: int,
                        out: Optional[torch.Tensor] = None, eps: float = 1e-6) -> torch.Tensor:
@@ -307,6 +333,18 @@ def linear_qkv_i8(xq, sx, wq, sw, b, qkv, rows_per_batch: int, seq_offset: int):
     _chk(M == B * rows_per_batch and seq_offset + rows_per_batch <= S_pad, "i8 qkv rows")
     _lib.call("qie_linear_qkv_i8", _p(xq), xq.stride(0), _p(sx), _p(wq), _p(sw), _p(b), _p(qkv), M, K,
               rows_per_batch, seq_offset, B, H, Dh, S_pad, _stream())
+
+
+def linear_qkv_norm_rope_i8(xq, sx, wq8, sw, b, qkv, rows_per_batch: int, seq_offset: int, wq, wk,
+                            cos_tab, sin_tab, eps: float = 1e-6):
+    M, K = xq.shape
+    _, B, H, S_pad, Dh = qkv.shape
+    _chk(xq.dtype == torch.int8 and wq8.shape == (3 * H * Dh, K) and K % 128 == 0, "i8 qkv")
+    _chk(M == B * rows_per_batch and seq_offset + rows_per_batch <= S_pad, "i8 qkv rows")
+    _rope_chk(qkv, rows_per_batch, wq, wk, cos_tab, sin_tab)
+    _lib.call("qie_linear_qkv_norm_rope_i8", _p(xq), xq.stride(0), _p(sx), _p(wq8), _p(sw), _p(b), _p(qkv), M,
+              K, rows_per_batch, seq_offset, B, H, Dh, S_pad, _p(wq), _p(wk), _p(cos_tab), _p(sin_tab), eps,
+              _stream())
 
 
 # ---------------------------------------------------------------------------- split-K linears

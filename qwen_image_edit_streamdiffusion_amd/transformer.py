@@ -181,6 +181,9 @@ class QwenImageTransformer2DModel(nn.Module):
         # _block). False: everything on the caller's stream, in the same order (A/B switch).
         self.overlap_text_stream = True
         self._side: Optional[torch.cuda.Stream] = None
+        # image-stream QKV projection with the QK RMSNorm + RoPE in its epilogue (one launch);
+        # False: the GEMM, then qie_qk_norm_rope_bf16 (A/B switch)
+        self.fuse_qk_norm_rope = True
         # K % 64 requirement of the GEMM kernels for the small input projections
         if in_channels % 64 or joint_attention_dim % 64:
             raise NotImplementedError("in_channels and joint_attention_dim must be multiples of 64")
@@ -529,17 +532,25 @@ class QwenImageTransformer2DModel(nn.Module):
         D = self.config.inner_dim
         ops.gemv(ws.stemb, getattr(blk, f"w_mod_{s}"), getattr(blk, f"b_mod_{s}"), out=m)
         # chunks of m: shift1 scale1 gate1 shift2 scale2 gate2
+        nq, nk = (blk.norm_q, blk.norm_k) if s == "img" else (blk.norm_added_q, blk.norm_added_k)
         if self.int8:
             qD, sc = self._q8(ws, s, x.shape[0], D)
             ops.layernorm_modulate_i8(x, m[:, 0:D], m[:, D:2 * D], rpb, qD, sc, eps)
-            self._linear(ws, blk, s, "qkv", (qD, sc), ops.EPI_QKV, ws.qkv, rpb=rpb, seq_off=seq_off)
+            inp = (qD, sc)
         else:
             ops.layernorm_modulate(x, m[:, 0:D], m[:, D:2 * D], rpb, out=h, eps=eps)
-            self._linear(ws, blk, s, "qkv", h, ops.EPI_QKV, ws.qkv, rpb=rpb, seq_off=seq_off)
-        if s == "img":
-            ops.qk_norm_rope(ws.qkv, seq_off, rpb, blk.norm_q, blk.norm_k, cos, sin, eps)
-        else:
-            ops.qk_norm_rope(ws.qkv, seq_off, rpb, blk.norm_added_q, blk.norm_added_k, cos, sin, eps)
+            inp = h
+        if s == "img" and self.fuse_qk_norm_rope:  # one launch: GEMM + per-head RMSNorm + RoPE
+            if self.int8:
+                wq8, sw = blk.q8["qkv_img"]
+                ops.linear_qkv_norm_rope_i8(qD, sc, wq8, sw, blk.b_qkv_img, ws.qkv, rpb, seq_off, nq, nk, cos,
+                                            sin, eps)
+            else:
+                ops.linear_qkv_norm_rope(h, blk.w_qkv_img, blk.b_qkv_img, ws.qkv, rpb, seq_off, nq, nk, cos,
+                                         sin, eps)
+            return
+        self._linear(ws, blk, s, "qkv", inp, ops.EPI_QKV, ws.qkv, rpb=rpb, seq_off=seq_off)
+        ops.qk_norm_rope(ws.qkv, seq_off, rpb, nq, nk, cos, sin, eps)
 
     def _stream_post(self, blk: _Block, ws: _Workspace, st, eps):
         """x += gate1 (att W_out + b); h = LN2(x)(1 + scale2) + shift2;

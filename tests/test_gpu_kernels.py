@@ -154,6 +154,61 @@ def test_qk_norm_rope(dev):
     assert torch.equal(qkv[:, :, :, S_img + txt:], orig[:, :, :, S_img + txt:])
 
 
+def _qkv_nr_case(dev, B, rpb, H, K, off, s_pad, seed, hw):
+    from qwen_image_edit_streamdiffusion_amd.rope import rope_tables
+    x = rnd((B * rpb, K), dev, 1.0, seed)
+    w, b = rnd((3 * H * 128, K), dev, 0.05, seed + 1), rnd((3 * H * 128,), dev, 0.1, seed + 2)
+    nq, nk = [(1 + rnd((128,), dev, 0.1, seed + 3 + i).float()).to(BF16) for i in range(2)]
+    shapes = [(1,) + hw, (1,) + hw]
+    assert 2 * hw[0] * hw[1] == rpb
+    ic, is_, _, _ = rope_tables(shapes, 16, dev)
+    return x, w, b, nq, nk, ic, is_, shapes
+
+
+@pytest.mark.parametrize("B,rpb,H,K,off,s_pad,hw", [
+    (2, 2048, 8, 256, 0, 2304, (32, 32)),    # 192 big tiles: the fused gemm_pp epilogue
+    (1, 4096, 16, 384, 0, 4352, (32, 64)),   # 16 x 24 tiles, K = 3 tiles
+    (2, 200, 2, 128, 40, 512, (10, 10)),     # small: GEMM + qie_qk_norm_rope_bf16 fallback
+])
+def test_qkv_norm_rope_fused(dev, B, rpb, H, K, off, s_pad, hw):
+    """QKV projection with QK RMSNorm + RoPE in the epilogue == the two-launch path (within the
+    GEMM tolerance: only the fp32 order of the sum of squares differs) and the oracle."""
+    ops = _ops()
+    x, w, b, nq, nk, ic, is_, shapes = _qkv_nr_case(dev, B, rpb, H, K, off, s_pad, 70, hw)
+    fused = torch.zeros(3, B, H, s_pad, 128, dtype=BF16, device=dev)
+    ops.linear_qkv_norm_rope(x, w, b, fused, rpb, off, nq, nk, ic, is_)
+    two = torch.zeros_like(fused)
+    ops.linear_qkv(x, w, b, two, rpb, off)
+    ops.qk_norm_rope(two, off, rpb, nq, nk, ic, is_)
+    sl = slice(off, off + rpb)
+    close(fused[:, :, :, sl], two[:, :, :, sl])
+    assert torch.equal(fused[2], two[2])  # V: no norm, same GEMM epilogue
+    assert (fused[:, :, :, :off] == 0).all() and (fused[:, :, :, off + rpb:] == 0).all()
+    lin = R.linear(x.cpu(), w.cpu(), b.cpu(), RB).view(B, rpb, 3, H, 128)
+    ip, _ = R.rope_phases(shapes, 16)
+    for which, wn in ((0, nq), (1, nk)):
+        ref = R.apply_rope(R.rms_norm(lin[:, :, which], wn.cpu(), 1e-6, RB), ip, RB).permute(0, 2, 1, 3)
+        close(fused[which, :, :, sl], ref, rel_l2=8e-3, ulps=4)
+
+
+def test_qkv_norm_rope_fused_i8(dev):
+    ops = _ops()
+    B, rpb, H, K = 2, 2048, 8, 256
+    g = torch.Generator().manual_seed(72)
+    xq = torch.randint(-127, 128, (B * rpb, K), generator=g, dtype=torch.int8).to(dev)
+    sx = (torch.rand(B * rpb, generator=g) * 0.01 + 1e-3).to(dev)
+    wq8 = torch.randint(-127, 128, (3 * H * 128, K), generator=g, dtype=torch.int8).to(dev)
+    sw = (torch.rand(3 * H * 128, generator=g) * 1e-3 + 1e-4).to(dev)
+    _, _, b, nq, nk, ic, is_, _ = _qkv_nr_case(dev, B, rpb, H, K, 0, 2304, 73, (32, 32))
+    fused = torch.zeros(3, B, H, 2304, 128, dtype=BF16, device=dev)
+    ops.linear_qkv_norm_rope_i8(xq, sx, wq8, sw, b, fused, rpb, 0, nq, nk, ic, is_)
+    two = torch.zeros_like(fused)
+    ops.linear_qkv_i8(xq, sx, wq8, sw, b, two, rpb, 0)
+    ops.qk_norm_rope(two, 0, rpb, nq, nk, ic, is_)
+    close(fused[:, :, :, :rpb], two[:, :, :, :rpb])
+    assert torch.equal(fused[2], two[2])
+
+
 def _attn_ref(qkv, kv_len, s_img, txt_rows):
     _, B, H, s_pad, Dh = qkv.shape
     S = s_img + txt_rows

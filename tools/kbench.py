@@ -67,6 +67,30 @@ def bench_gemm(name, M, N, K, kind):
     return f"{name} M={M} N={N} K={K}: {ms:.3f} ms  {2.0 * M * N * K / ms / 1e9:.0f} TFLOP/s"
 
 
+def bench_qkv_variants():
+    """QKV projection at the image-stream shape: plain GEMM, QKV scatter, scatter + separate
+    QK-norm/RoPE kernel, and the fused epilogue (same process, same inputs)."""
+    from qwen_image_edit_streamdiffusion_amd.rope import rope_tables
+    M, N, K = B * S_IMG, 3 * D, D
+    x, w, b = rnd(M, K), rnd(N, K, scale=0.02), rnd(N, scale=0.02)
+    s_pad = ((S_IMG + S_TXT + 255) // 256) * 256
+    qkv = torch.zeros(3, B, H, s_pad, 128, dtype=BF16, device=dev)
+    y = torch.empty(M, N, dtype=BF16, device=dev)
+    ic, is_, _, _ = rope_tables([(1, 64, 64), (1, 64, 64)], S_TXT, dev)
+    nw = rnd(128)
+    fl = 2.0 * M * N * K
+    out = []
+    for name, fn in (("qkv_plain", lambda: ops.linear(x, w, b, out=y)),
+                     ("qkv_scatter", lambda: ops.linear_qkv(x, w, b, qkv, S_IMG, 0)),
+                     ("qkv_scatter+norm_rope", lambda: (ops.linear_qkv(x, w, b, qkv, S_IMG, 0),
+                                                        ops.qk_norm_rope(qkv, 0, S_IMG, nw, nw, ic, is_))),
+                     ("qkv_fused_norm_rope", lambda: ops.linear_qkv_norm_rope(x, w, b, qkv, S_IMG, 0, nw, nw,
+                                                                              ic, is_))):
+        ms = timeit(fn)
+        out.append(f"{name} M={M} N={N} K={K}: {ms:.3f} ms  {fl / ms / 1e9:.0f} TFLOP/s")
+    return out
+
+
 def bench_i8(name, M, N, K, act=0):
     xq = torch.randint(-127, 128, (M, K), dtype=torch.int8, device=dev)
     wq = torch.randint(-127, 128, (N, K), dtype=torch.int8, device=dev)
@@ -130,6 +154,8 @@ def main():
         M = B * S_IMG
         res.append(bench_i8("i8_up", M, F, D, act=1))
         res.append(bench_i8("i8_down", M, D, F))
+    if not want or "qkv" in want:
+        res += bench_qkv_variants()
     if not want or "misc" in want:
         res += bench_misc()
     for r in res:
