@@ -64,6 +64,9 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 // the end of an M-phase (this wave's pieces from its previous V-phase), vmcnt(pieces) at the
 // end of a V-phase; one barrier per phase.
 constexpr int kRing = 3;
+#ifndef QIE_ATTN_ABL  // diagnostic ablations (wrong results): 1 no K/V DMA in the loop, 2 no exp2
+#define QIE_ATTN_ABL 0
+#endif
 
 #ifdef QIE_ATTN_STAMP
 // diagnostic build only (tools/attn_stamp.hip): per-group sums of phase cycles
@@ -247,8 +250,10 @@ __global__ void __launch_bounds__(512) attn_pp_kernel(AttnArgs a) {
 #pragma unroll
     for (int db = 0; db < 4; ++db) rfence(st.o[db]);
     int pieces = 0;
-    if (t + 2 < ntiles) { dmaK(t + 2); pieces += 2; }
-    if (t + 1 < ntiles) { dmaV(t + 1); pieces += 2; }
+    if (!(QIE_ATTN_ABL & 1)) {
+      if (t + 2 < ntiles) { dmaK(t + 2); pieces += 2; }
+      if (t + 1 < ntiles) { dmaV(t + 1); pieces += 2; }
+    }
     const int kv0 = t * kKB;
     if (kv0 + kKB > kv_len) {
 #pragma unroll
@@ -281,8 +286,13 @@ __global__ void __launch_bounds__(512) attn_pp_kernel(AttnArgs a) {
     for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
       for (int r = 0; r < 16; r += 2) {
+#if QIE_ATTN_ABL & 2
+        const float p0 = __builtin_fmaf(st.s[cb][r], c, -mc);
+        const float p1 = __builtin_fmaf(st.s[cb][r + 1], c, -mc);
+#else
         const float p0 = __builtin_amdgcn_exp2f(__builtin_fmaf(st.s[cb][r], c, -mc));
         const float p1 = __builtin_amdgcn_exp2f(__builtin_fmaf(st.s[cb][r + 1], c, -mc));
+#endif
         ps0 += p0;
         ps1 += p1;
         st.pf[cb * 2 + (r >> 3)][r & 7] = (__bf16)p0;

@@ -347,6 +347,9 @@ constexpr int kRingNT = QIE_RING_NT;
 #ifndef QIE_GEMM_PP  // 1: gemm_pp_kernel for the big shapes (+14 % over gemm_ring in A/B); 0: gemm_ring
 #define QIE_GEMM_PP 1
 #endif
+#ifndef QIE_SPLITK_PP  // 1: split-K partials on gemm_pp tiles (256x256), 0: on gemm_kernel<128,128>
+#define QIE_SPLITK_PP 1
+#endif
 #ifndef QIE_PP_ABL  // diagnostic ablations of gemm_pp (wrong results): 1 no DMA, 2 no LDS reads
 #define QIE_PP_ABL 0
 #endif
@@ -424,6 +427,18 @@ __device__ __forceinline__ void ring_epilogue(typename MfmaOp<I8>::acc (&acc)[8]
                  : "+a"(acc[7][0]), "+a"(acc[7][1]), "+a"(acc[7][2]), "+a"(acc[7][3]), "+a"(acc[6][0]),
                    "+a"(acc[6][1]), "+a"(acc[6][2]), "+a"(acc[6][NT - 1]));
   const int g = lane >> 4, fr = lane & 15;
+  if constexpr (EPI == EPI_PARTIAL) {  // raw fp32 / int32 partial sums of split blockIdx.y
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int m = mrow0 + i * 16 + fr;
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const int n = ncol0 + j * 16 + g * 4;
+        if (m < M && n < N) *(typename MfmaOp<I8>::acc*)((char*)e.ws + (((int64_t)blockIdx.y * M + m) * N + n) * 4) = acc[i][j];
+      }
+    }
+    return;
+  }
   constexpr bool QKV = EPI == EPI_QKV || EPI == EPI_QKV_NR;
   if constexpr (QKV && NT == 4) {
     if (EPI == EPI_QKV_NR || e.head_dim == 128) {
@@ -522,7 +537,7 @@ __device__ __forceinline__ void ring_epilogue(typename MfmaOp<I8>::acc (&acc)[8]
       return;
     }
   }
-  if constexpr (EPI != EPI_QKV_NR) {
+  if constexpr (EPI != EPI_QKV_NR && EPI != EPI_PARTIAL) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int m = mrow0 + i * 16 + fr;
@@ -750,7 +765,11 @@ __device__ __forceinline__ void pp_dma(const i32x4_t& r, const char QIE_LDS* dst
 }
 
 constexpr int kPPTile = 256 * kRowBytes;  // one operand of one K tile, 32 KiB
-constexpr int kPPBuf = 2 * kPPTile;       // X + W, 64 KiB; two buffers
+#ifndef QIE_PP_XRING  // X tiles in flight + 1: 2 -> 128 KiB of LDS, 3 -> all 160 KiB
+#define QIE_PP_XRING 2
+#endif
+constexpr int kPPX = QIE_PP_XRING;        // X slots; W always has 2
+constexpr int kPPXA = kPPX - 1;           // X(k + kPPXA) is staged during tile k
 
 template <int EPI, bool I8>
 __global__ void __launch_bounds__(512, 2)
@@ -759,7 +778,7 @@ __global__ void __launch_bounds__(512, 2)
   using frag = typename MfmaOp<I8>::frag;
   using accT = typename MfmaOp<I8>::acc;
   constexpr int NT = 4, NWAVE = 8, PPO = 4;  // PPO: DMA pieces per wave per operand tile
-  __shared__ __attribute__((aligned(16))) char smem_raw[2 * kPPBuf];
+  __shared__ __attribute__((aligned(16))) char smem_raw[(kPPX + 2) * kPPTile];
   char QIE_LDS* smem = (char QIE_LDS*)smem_raw;
 
   const int tiles_m = (M + 255) >> 8, tiles_n = (N + 255) >> 8;
@@ -778,8 +797,10 @@ __global__ void __launch_bounds__(512, 2)
   const int m_valid = M - m0, n_valid = N - n0;
   const int nk = K_bytes / kRowBytes;  // host guarantees nk >= 3
 
-  const i32x4_t xr = pp_rsrc(X + (int64_t)m0 * ldx_b, (int)(min(m_valid, 256) * ldx_b));
-  const i32x4_t wr = pp_rsrc(W + (int64_t)n0 * ldw_b, (int)(min(n_valid, 256) * ldw_b));
+  // split-K (EPI_PARTIAL): blockIdx.y selects a K range of K_bytes (gridDim.y == 1 otherwise)
+  const int64_t koff = (int64_t)blockIdx.y * K_bytes;
+  const i32x4_t xr = pp_rsrc(X + (int64_t)m0 * ldx_b + koff, (int)(min(m_valid, 256) * ldx_b - koff));
+  const i32x4_t wr = pp_rsrc(W + (int64_t)n0 * ldw_b + koff, (int)(min(n_valid, 256) * ldw_b - koff));
   // piece i of an operand tile: rows 8 (wave + 8 i) .. +7, lane -> row + (lane >> 3), swizzled chunk
   uint32_t xo[PPO], wo[PPO];
 #pragma unroll
@@ -789,24 +810,21 @@ __global__ void __launch_bounds__(512, 2)
     xo[i] = (uint32_t)(min(r, m_valid - 1) * ldx_b) + (c << 4);
     wo[i] = (uint32_t)(min(r, n_valid - 1) * ldw_b) + (c << 4);
   }
-  auto dmaX = [&](int kt, int i) {
-    pp_dma(xr, smem + (kt & 1) * kPPBuf + (wave + i * NWAVE) * 1024, xo[i], kt * kRowBytes);
-  };
-  auto dmaW = [&](int kt, int i) {
-    pp_dma(wr, smem + (kt & 1) * kPPBuf + kPPTile + (wave + i * NWAVE) * 1024, wo[i], kt * kRowBytes);
-  };
+  // LDS: X slots [0, kPPX) (tile kt in slot kt % kPPX), then two W slots (tile kt in kt & 1)
+  auto xslot = [&](int kt) { return smem + (kt % kPPX) * kPPTile; };
+  auto wslot = [&](int kt) { return smem + (kPPX + (kt & 1)) * kPPTile; };
+  auto dmaX = [&](int kt, int i) { pp_dma(xr, xslot(kt) + (wave + i * NWAVE) * 1024, xo[i], kt * kRowBytes); };
+  auto dmaW = [&](int kt, int i) { pp_dma(wr, wslot(kt) + (wave + i * NWAVE) * 1024, wo[i], kt * kRowBytes); };
 
   // fragment of k-step ks: lane reads row (lane & 15) of its 16-row block, chunk 4 ks + (lane >> 4)
   const int fr = lane & 15;
   const int a_row = wm * 128 + fr, w_row = wn * NT * 16 + fr;
   const int sw = (fr >> 1) & 7;  // swz_chunk term; (row + 16 i) >> 1 & 7 == row >> 1 & 7
   auto ldX = [&](int kt, int i, int ks) -> frag {
-    return *(const frag QIE_LDS*)(smem + (kt & 1) * kPPBuf + (a_row + 16 * i) * kRowBytes +
-                                  (((4 * ks + (lane >> 4)) ^ sw) << 4));
+    return *(const frag QIE_LDS*)(xslot(kt) + (a_row + 16 * i) * kRowBytes + (((4 * ks + (lane >> 4)) ^ sw) << 4));
   };
   auto ldW = [&](int kt, int j, int ks) -> frag {
-    return *(const frag QIE_LDS*)(smem + (kt & 1) * kPPBuf + kPPTile + (w_row + 16 * j) * kRowBytes +
-                                  (((4 * ks + (lane >> 4)) ^ sw) << 4));
+    return *(const frag QIE_LDS*)(wslot(kt) + (w_row + 16 * j) * kRowBytes + (((4 * ks + (lane >> 4)) ^ sw) << 4));
   };
 
   accT acc[8][NT];
@@ -837,8 +855,8 @@ __global__ void __launch_bounds__(512, 2)
     }
     if constexpr (!(QIE_PP_ABL & 1)) {
       if constexpr (DX) {
-        dmaX(kt + 1, 2 * KS);
-        dmaX(kt + 1, 2 * KS + 1);
+        dmaX(kt + kPPXA, 2 * KS);
+        dmaX(kt + kPPXA, 2 * KS + 1);
       }
       if constexpr (DW) {
         dmaW(kt + 2, 2 * KS);
@@ -873,21 +891,34 @@ __global__ void __launch_bounds__(512, 2)
     section(I1{}, I1{}, init_t, F{}, dw_t, vm_t, kt);
   };
 
-  // prologue: W(0), X(0), W(1); wait for the first two; group 1 one barrier behind
+  // prologue (2 X slots): W(0), X(0), W(1); (3 X slots): X(0), W(0), X(1), W(1); wait for tile 0;
+  // group 1 one barrier behind. Steady tile k stages X(k + kPPXA) and W(k + 2) and waits for
+  // everything but its own pieces (vmcnt VS) -> tile k+1 has landed.
+  using VS = std::integral_constant<int, kPPXA == 1 ? 4 : 8>;
+  if constexpr (kPPXA == 1) {
 #pragma unroll
-  for (int i = 0; i < PPO; ++i) dmaW(0, i);
+    for (int i = 0; i < PPO; ++i) dmaW(0, i);
 #pragma unroll
-  for (int i = 0; i < PPO; ++i) dmaX(0, i);
+    for (int i = 0; i < PPO; ++i) dmaX(0, i);
+  } else {
+#pragma unroll
+    for (int i = 0; i < PPO; ++i) dmaX(0, i);
+#pragma unroll
+    for (int i = 0; i < PPO; ++i) dmaW(0, i);
+#pragma unroll
+    for (int i = 0; i < PPO; ++i) dmaX(1, i);
+  }
 #pragma unroll
   for (int i = 0; i < PPO; ++i) dmaW(1, i);
-  ld_end(V4{});
+  ld_end(VS{});
   if (wm == 1) asm volatile("s_barrier" ::: "memory");
 
-  tile(T{}, T{}, T{}, V4{}, 0);
+  tile(T{}, T{}, T{}, VS{}, 0);
   int kt = 1;
-  for (; kt < nk - 2; ++kt) tile(F{}, T{}, T{}, V4{}, kt);
-  tile(F{}, T{}, F{}, V0{}, kt);         // nk-2: stages X(nk-1), waits for it
-  tile(F{}, F{}, F{}, VNone{}, kt + 1);  // nk-1
+  for (; kt < nk - 2; ++kt) tile(F{}, T{}, T{}, VS{}, kt);
+  if constexpr (kPPXA == 1) tile(F{}, T{}, F{}, V0{}, kt);  // nk-2: stages X(nk-1), waits for it
+  else tile(F{}, F{}, F{}, V0{}, kt);                       // nk-2: waits for tile nk-1
+  tile(F{}, F{}, F{}, VNone{}, kt + 1);                     // nk-1
   if (wm == 0) asm volatile("s_barrier" ::: "memory");  // every wave passes the same barrier count
 
   ring_epilogue<NT, EPI, I8>(acc, e, M, N, m0 + wm * 128, n0 + wn * NT * 16, lane, smem);
@@ -966,10 +997,17 @@ int launch_splitk(const void* x, int64_t ldx, const void* w, int M, int N, int K
   QIE_CHECK_ARG(((ldx * eb) % 16) == 0 && ((uintptr_t)x % 16) == 0 && ((uintptr_t)w % 16) == 0);
   QIE_CHECK_ARG(((uintptr_t)e.ws % 16) == 0 && ws_bytes >= (int64_t)splits * M * N * 4);
   const int kb = K * eb / splits;
-  const dim3 grid(((M + 127) / 128) * ((N + 127) / 128), splits);
-  gemm_kernel<128, 128, 2, 2, EPI_PARTIAL, I8><<<grid, 256, 0, s>>>((const char*)x, ldx * eb,
-                                                                   (const char*)w, (int64_t)K * eb,
-                                                                   M, N, kb, e);
+  if (QIE_GEMM_PP && QIE_SPLITK_PP && M >= 128 && N >= 256 && kb >= 3 * kRowBytes) {
+    // 256x256 ping-pong tiles (the text stream: M = B * S_txt ~ 432 -> 2 row tiles)
+    const dim3 grid(((M + 255) / 256) * ((N + 255) / 256), splits);
+    gemm_pp_kernel<EPI_PARTIAL, I8><<<grid, 512, 0, s>>>((const char*)x, ldx * eb, (const char*)w,
+                                                        (int64_t)K * eb, M, N, kb, e);
+  } else {
+    const dim3 grid(((M + 127) / 128) * ((N + 127) / 128), splits);
+    gemm_kernel<128, 128, 2, 2, EPI_PARTIAL, I8><<<grid, 256, 0, s>>>((const char*)x, ldx * eb,
+                                                                     (const char*)w, (int64_t)K * eb,
+                                                                     M, N, kb, e);
+  }
   const int64_t nq = (int64_t)M * (N / 4);
   const int nb = (int)((nq + 255) / 256);
   switch (epi_kind) {

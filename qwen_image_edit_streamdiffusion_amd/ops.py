@@ -354,13 +354,14 @@ EPI_BIAS, EPI_GELU, EPI_GATED_RESIDUAL, EPI_QKV = (_lib.EPI_BIAS, _lib.EPI_GELU,
 def splitk_splits(N: int, K: int, int8: bool = False) -> int:
     """K-range count for the text-stream (short-M) linears. A function of (N, K) only -- never
     of M -- so a row's arithmetic is the same at every batch size (batched CFG == sequential).
-    Aims at >= ~768 work-groups for M ~ 432 (4 row tiles) with >= 12 K-steps per range."""
+    Sized for the 256x256 gemm_pp tiles: M ~ 432 is 2 row tiles, so 2 * ceil(N / 256) tiles x
+    splits should stay within one round of the 256 CUs, with >= 12 K tiles (128 B) per range."""
     steps = (K * (1 if int8 else 2)) // 128
-    want = max(1, -(-768 // (4 * max(1, -(-N // 128)))))
-    s = 1
-    while s < want and steps % (2 * s) == 0 and steps // (2 * s) >= 12:
-        s *= 2
-    return s
+    tiles = 2 * -(-N // 256)
+    for s in range(min(max(1, 256 // tiles), steps // 12), 1, -1):
+        if steps % s == 0:
+            return s
+    return 1
 
 
 def splitk_workspace_bytes(M: int, N: int, splits: int) -> int:

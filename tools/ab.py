@@ -25,6 +25,9 @@ def load(path):
     if hasattr(lib, "qie_attention_fwd_split_bf16"):
         lib.qie_attention_fwd_split_bf16.argtypes = lib.qie_attention_fwd_bf16.argtypes[:-1] + [
             ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
+    lib.qie_linear_splitk_bf16.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
+                                           ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                           ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
     lib.qie_linear_bf16.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
                                     ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                     ctypes.c_int, ctypes.c_void_p]
@@ -45,6 +48,8 @@ def main():
         s_pad = ((S + 255) // 256) * 256
         qkv = torch.randn(3, B, H, s_pad, 128, device=dev).to(BF16)
         qkv[:, :, :, S:] = 0
+        if os.environ.get("AB_ZERO"):
+            qkv.zero_()
         outs = [(torch.empty(B * S_IMG, H * 128, dtype=BF16, device=dev),
                  torch.empty(B * S_TXT, H * 128, dtype=BF16, device=dev)) for _ in libs]
         kv = (ctypes.c_int * B)(*[S] * B)
@@ -61,6 +66,23 @@ def main():
             else:
                 rc = lib.qie_attention_fwd_bf16(qkv.data_ptr(), B, H, s_pad, kv, outs[i][0].data_ptr(),
                                                 outs[i][1].data_ptr(), S_IMG, S_TXT, 1 / math.sqrt(128), st)
+            assert rc == 0, rc
+    elif what.startswith("splitk:"):  # splitk:M:N:K:s_lib0:s_lib1:... (split count per library)
+        parts = [int(v) for v in what.split(":")[1:]]
+        M, N, K, spl = parts[0], parts[1], parts[2], parts[3:]
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        from qwen_image_edit_streamdiffusion_amd import _lib as L
+        x = torch.randn(M, K, device=dev).to(BF16)
+        w = (torch.randn(N, K, device=dev) * 0.02).to(BF16)
+        b = torch.zeros(N, device=dev, dtype=BF16)
+        outs = [torch.empty(M, N, dtype=BF16, device=dev) for _ in libs]
+        ws = torch.empty(max(spl) * M * N, device=dev)
+        eps = [L.Epilogue(kind=0, out=o.data_ptr(), ldo=N) for o in outs]
+        flops = 2.0 * M * N * K
+
+        def run(i):
+            rc = libs[i].qie_linear_splitk_bf16(x.data_ptr(), K, w.data_ptr(), b.data_ptr(), ctypes.addressof(eps[i]),
+                                                M, N, K, spl[i], ws.data_ptr(), ws.numel() * 4, st)
             assert rc == 0, rc
     elif what.startswith("gemm"):
         if what.startswith("gemm:"):  # gemm:M:N:K

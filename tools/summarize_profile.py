@@ -21,8 +21,8 @@ import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KEYS = {"attention": "attn_pp_kernel", "mlp_up": "gemm_ring_kernel<4, 1, false>",
-        "gated_gemm": "gemm_ring_kernel<4, 2, false>", "qkv_gemm": "gemm_ring_kernel<4, 3, false>"}
+KEYS = {"attention": "attn_pp_kernel", "mlp_up": "gemm_pp_kernel<1, false>",
+        "gated_gemm": "gemm_pp_kernel<2, false>", "qkv_gemm": "gemm_pp_kernel<5, false>"}
 
 
 def main():
