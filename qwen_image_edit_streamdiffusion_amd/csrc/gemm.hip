@@ -537,6 +537,50 @@ __device__ __forceinline__ void ring_epilogue(typename MfmaOp<I8>::acc (&acc)[8]
       return;
     }
   }
+  if constexpr (EPI == EPI_GATE_RES && NT == 4) {
+    // x is read and written in place, so hipcc cannot hoist a later row's residual load above an
+    // earlier row's store: issue the residual and gate loads of 4 rows first, then combine and
+    // store (one round trip per 4 rows instead of one per 16-byte chunk)
+#pragma unroll
+    for (int h2 = 0; h2 < 2; ++h2) {
+      u32x4_t xv[4][2], gv[4][2];
+#pragma unroll
+      for (int ii = 0; ii < 4; ++ii) {
+        const int mc = min(mrow0 + (4 * h2 + ii) * 16 + fr, M - 1);
+        const int b = mc / e.rows_per_batch;
+#pragma unroll
+        for (int jp = 0; jp < 2; ++jp) {
+          const int n = min(ncol0 + jp * 32 + (g & 1) * 16 + (g >> 1) * 8, N - 8);
+          xv[ii][jp] = *(const u32x4_t*)((const bf16_t*)e.out + (int64_t)mc * e.ldo + n);
+          gv[ii][jp] = *(const u32x4_t*)(e.gate + (int64_t)b * e.gate_bstride + n);
+        }
+      }
+#pragma unroll
+      for (int ii = 0; ii < 4; ++ii) {
+        const int i = 4 * h2 + ii;
+        const int m = mrow0 + i * 16 + fr;
+        const int mc = min(m, M - 1);
+#pragma unroll
+        for (int jp = 0; jp < 2; ++jp) {
+          const int nb = ncol0 + jp * 32;
+          u32x2_t a = epi_pre<EPI, I8>(e, mc, min(nb + g * 4, N - 4), acc[i][2 * jp]);
+          u32x2_t b = epi_pre<EPI, I8>(e, mc, min(nb + 16 + g * 4, N - 4), acc[i][2 * jp + 1]);
+          const auto sx = __builtin_amdgcn_permlane16_swap(a.x, b.x, false, false);
+          const auto sy = __builtin_amdgcn_permlane16_swap(a.y, b.y, false, false);
+          const uint32_t vv[4] = {sx[0], sy[0], sx[1], sy[1]};
+          const uint32_t gg[4] = {gv[ii][jp].x, gv[ii][jp].y, gv[ii][jp].z, gv[ii][jp].w};
+          const uint32_t xx[4] = {xv[ii][jp].x, xv[ii][jp].y, xv[ii][jp].z, xv[ii][jp].w};
+          uint32_t o[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            o[k] = pack2(lo_f(xx[k]) + rbf(lo_f(gg[k]) * lo_f(vv[k])), hi_f(xx[k]) + rbf(hi_f(gg[k]) * hi_f(vv[k])));
+          const int n = nb + (g & 1) * 16 + (g >> 1) * 8;
+          if (m < M && n < N) *(u32x4_t*)((bf16_t*)e.out + (int64_t)m * e.ldo + n) = u32x4_t{o[0], o[1], o[2], o[3]};
+        }
+      }
+    }
+    return;
+  }
   if constexpr (EPI != EPI_QKV_NR && EPI != EPI_PARTIAL) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) {

@@ -84,6 +84,23 @@ def main():
             rc = libs[i].qie_linear_splitk_bf16(x.data_ptr(), K, w.data_ptr(), b.data_ptr(), ctypes.addressof(eps[i]),
                                                 M, N, K, spl[i], ws.data_ptr(), ws.numel() * 4, st)
             assert rc == 0, rc
+    elif what.startswith("gate:"):  # gate:M:N:K -- gated-residual epilogue (resid += gate * y)
+        M, N, K = (int(v) for v in what.split(":")[1:])
+        x = torch.randn(M, K, device=dev).to(BF16)
+        w = (torch.randn(N, K, device=dev) * 0.02).to(BF16)
+        b = torch.zeros(N, device=dev, dtype=BF16)
+        gate = (torch.randn(2, 6 * N, device=dev) * 0.1).to(BF16)
+        outs = [torch.randn(M, N, device=dev).to(BF16) for _ in libs]
+        flops = 2.0 * M * N * K
+        for lib in libs:
+            lib.qie_linear_gated_residual_bf16.argtypes = [
+                ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+
+        def run(i):
+            rc = libs[i].qie_linear_gated_residual_bf16(x.data_ptr(), K, w.data_ptr(), b.data_ptr(), gate.data_ptr(),
+                                                        6 * N, M // 2, outs[i].data_ptr(), N, M, N, K, st)
+            assert rc == 0, rc
     elif what.startswith("gemm"):
         if what.startswith("gemm:"):  # gemm:M:N:K
             M, N, K = (int(v) for v in what.split(":")[1:])
