@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define QIE_ABI_VERSION 1
+#define QIE_ABI_VERSION 2
 #define QIE_MAX_BATCH 16
 
 #define QIE_OK 0
@@ -99,22 +99,24 @@ int qie_rmsnorm_bf16(const void* x, const void* w, void* y, int rows, int D, flo
 /* K7 -- attn.norm_q/norm_k (or norm_added_q/k) RMSNorm(head_dim) followed by
  * apply_rotary_emb_qwen(use_real=False) [U], in place on sequence rows
  * [seg_start, seg_start + seg_len) of the Q and K planes of the joint buffer.
- * cos_tab/sin_tab: fp32 [seg_len][head_dim/2] rows for that segment. */
+ * cos_tab/sin_tab: fp32 [seg_len][head_dim/2] rows for that segment.
+ * q_scale multiplies the rotated q rows before their single bf16 rounding (1.0: the plain op;
+ * scale * log2(e) feeds qie_attention_fwd_log2q_bf16); k rows are unscaled. */
 int qie_qk_norm_rope_bf16(void* qkv, int batch, int heads, int head_dim, int s_pad, int seg_start,
                           int seg_len, const void* wq, const void* wk, const float* cos_tab,
-                          const float* sin_tab, float eps, qie_stream_t stream);
+                          const float* sin_tab, float eps, float q_scale, qie_stream_t stream);
 
 /* K1 + K7 fused -- the q|k|v projection of one stream (as qie_linear_qkv_bf16) followed by
  * attn.norm_q/norm_k (norm_added_q/k) RMSNorm(head_dim) and apply_rotary_emb_qwen [U] on its q
  * and k rows, with the rounding points of qie_qk_norm_rope_bf16. head_dim == 128; cos_tab /
  * sin_tab: fp32 [rows_per_batch][64] for this stream's segment. Big shapes run as ONE GEMM
  * whose epilogue normalises and rotates each head (the two halves of a head meet through LDS);
- * other shapes run the GEMM and then qie_qk_norm_rope_bf16. */
+ * other shapes run the GEMM and then qie_qk_norm_rope_bf16. q_scale as there. */
 int qie_linear_qkv_norm_rope_bf16(const void* x, int64_t ldx, const void* w, const void* bias, void* qkv,
                                   int M, int K, int rows_per_batch, int seq_offset, int batch, int heads,
                                   int head_dim, int s_pad, const void* wq, const void* wk,
                                   const float* cos_tab, const float* sin_tab, float eps,
-                                  qie_stream_t stream);
+                                  float q_scale, qie_stream_t stream);
 
 /* ------------------------------------------------------------------ attention */
 
@@ -143,6 +145,16 @@ int qie_attention_fwd_split_bf16(const void* qkv, int batch, int heads, int s_pa
                                  const int* kv_len_host, void* out_img, void* out_txt, int s_img,
                                  int txt_rows, float scale, void* workspace,
                                  int64_t workspace_bytes, qie_stream_t stream);
+
+/* The same SDPA for a q plane that already holds q * scale * log2(e) -- the producers fold that
+ * factor in before their single bf16 rounding (q_scale of qie_qk_norm_rope_bf16 /
+ * qie_linear_qkv_norm_rope_*). The logits then come out of the MFMA in log2 units, offset by
+ * the running max (the first MFMA's C operand), and the softmax skips one multiply-add per
+ * score. workspace may be NULL (no split); otherwise as qie_attention_fwd_split_bf16. */
+int qie_attention_fwd_log2q_bf16(const void* qkv, int batch, int heads, int s_pad,
+                                 const int* kv_len_host, void* out_img, void* out_txt, int s_img,
+                                 int txt_rows, void* workspace, int64_t workspace_bytes,
+                                 qie_stream_t stream);
 
 /* ------------------------------------------------------------------ small ops */
 
@@ -208,12 +220,13 @@ int qie_linear_qkv_i8(const void* xq, int64_t ldx, const float* sx, const void* 
                       int rows_per_batch, int seq_offset, int batch, int heads, int head_dim,
                       int s_pad, qie_stream_t stream);
 
-/* qie_linear_qkv_norm_rope_bf16 on the int8 linear (dequant epilogue as qie_linear_qkv_i8). */
+/* qie_linear_qkv_norm_rope_bf16 on the int8 linear (dequant epilogue as qie_linear_qkv_i8),
+ * q_scale as there. */
 int qie_linear_qkv_norm_rope_i8(const void* xq, int64_t ldx, const float* sx, const void* wq,
                                 const float* sw, const void* bias, void* qkv, int M, int K,
                                 int rows_per_batch, int seq_offset, int batch, int heads, int head_dim,
                                 int s_pad, const void* nq, const void* nk, const float* cos_tab,
-                                const float* sin_tab, float eps, qie_stream_t stream);
+                                const float* sin_tab, float eps, float q_scale, qie_stream_t stream);
 
 /* ---- split-K linears for short-M shapes (the text stream, M = B * S_txt) ---------------------
  * Replaces the same diffusers linears as the entry points above (text-stream add_q/k/v_proj,

@@ -31,6 +31,8 @@ class Epilogue(ctypes.Structure):
 
 EPI_BIAS, EPI_GELU, EPI_GATED_RESIDUAL, EPI_QKV = 0, 1, 2, 3
 
+ABI_VERSION = 2  # include/qie.h QIE_ABI_VERSION
+
 # name -> argtypes (return type is always c_int unless listed in _RESTYPES)
 SIGNATURES = {
     "qie_abi_version": [],
@@ -38,14 +40,15 @@ SIGNATURES = {
     "qie_linear_bf16": [P, L, P, P, P, L, I, I, I, I, P],
     "qie_linear_gated_residual_bf16": [P, L, P, P, P, L, I, P, L, I, I, I, P],
     "qie_linear_qkv_bf16": [P, L, P, P, P, I, I, I, I, I, I, I, I, P],
-    "qie_linear_qkv_norm_rope_bf16": [P, L, P, P, P, I, I, I, I, I, I, I, I, P, P, P, P, F, P],
+    "qie_linear_qkv_norm_rope_bf16": [P, L, P, P, P, I, I, I, I, I, I, I, I, P, P, P, P, F, F, P],
     "qie_gemv_bf16": [P, L, P, P, P, L, I, I, I, P],
     "qie_layernorm_modulate_bf16": [P, L, P, P, L, I, P, L, I, I, F, P],
     "qie_rmsnorm_bf16": [P, P, P, I, I, F, P],
-    "qie_qk_norm_rope_bf16": [P, I, I, I, I, I, I, P, P, P, P, F, P],
+    "qie_qk_norm_rope_bf16": [P, I, I, I, I, I, I, P, P, P, P, F, F, P],
     "qie_attention_fwd_bf16": [P, I, I, I, IP, P, P, I, I, F, P],
     "qie_attention_workspace_bytes": [I, I, I, I, I, POINTER(c_int64)],
     "qie_attention_fwd_split_bf16": [P, I, I, I, IP, P, P, I, I, F, P, L, P],
+    "qie_attention_fwd_log2q_bf16": [P, I, I, I, IP, P, P, I, I, P, L, P],
     "qie_timestep_embed_bf16": [P, P, I, I, P],
     "qie_silu_bf16": [P, P, L, P],
     "qie_cfg_combine_bf16": [P, L, P, L, P, L, I, I, I, F, P],
@@ -58,7 +61,7 @@ SIGNATURES = {
     "qie_linear_i8": [P, L, P, P, P, P, P, L, I, I, I, I, P],
     "qie_linear_gated_residual_i8": [P, L, P, P, P, P, P, L, I, P, L, I, I, I, P],
     "qie_linear_qkv_i8": [P, L, P, P, P, P, P, I, I, I, I, I, I, I, I, P],
-    "qie_linear_qkv_norm_rope_i8": [P, L, P, P, P, P, P, I, I, I, I, I, I, I, I, P, P, P, P, F, P],
+    "qie_linear_qkv_norm_rope_i8": [P, L, P, P, P, P, P, I, I, I, I, I, I, I, I, P, P, P, P, F, F, P],
     "qie_linear_splitk_bf16": [P, L, P, P, P, I, I, I, I, P, L, P],
     "qie_linear_splitk_i8": [P, L, P, P, P, P, P, I, I, I, I, P, L, P],
 }
@@ -85,7 +88,7 @@ def load(path: str = LIB_PATH):
         fn = getattr(lib, name)
         fn.argtypes = args
         fn.restype = _RESTYPES.get(name, c_int)
-    if lib.qie_abi_version() != 1:
+    if lib.qie_abi_version() != ABI_VERSION:
         raise QieError("libqie.so ABI version mismatch")
     _lib = lib
     return lib

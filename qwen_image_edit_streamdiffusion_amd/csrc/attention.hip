@@ -109,6 +109,10 @@ __device__ __forceinline__ void mma32(f32x16_t& c, const bf16x8_t& a, const bf16
 __device__ __forceinline__ void mma32_z(f32x16_t& c, const bf16x8_t& a, const bf16x8_t& b) {
   asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(c) : "v"(a), "v"(b));
 }
+// first MFMA of a chain with a separate C operand (D = A.B + C0)
+__device__ __forceinline__ void mma32_c(f32x16_t& c, const bf16x8_t& a, const bf16x8_t& b, const f32x16_t& c0) {
+  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %3" : "=&v"(c) : "v"(a), "v"(b), "v"(c0));
+}
 template <typename T>
 __device__ __forceinline__ void rfence(T& x) {
   asm volatile("" : "+v"(x));
@@ -116,12 +120,19 @@ __device__ __forceinline__ void rfence(T& x) {
 
 struct PPState {
   f32x16_t s[2];
+  f32x16_t negm;  // PRE: splat(-m_run), the C operand of each tile's first QK^T MFMA
   f32x16_t o[4];
   bf16x8_t pf[4];
   bf16x8_t qf[8];
   float m_run, l_run;
 };
 
+// PRE: Q was written pre-multiplied by scale * log2(e) (the QKV epilogue folds it in before its
+// single bf16 rounding), so S^T holds log2-unit logits. Each tile's QK^T chain then starts from
+// C = -m_run and its accumulator is already the exponent: the softmax drops one v_fma_f32 per
+// score (32 per lane and tile, ~1/5 of the phase's VALU issue). The lazy rescale subtracts the
+// max growth from S in its (rare) branch; the first tile of a range always takes it.
+template <bool PRE>
 __global__ void __launch_bounds__(512) attn_pp_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) char smem_raw[2 * kRing * kTileBytes];  // K ring, V ring
   char QIE_LDS* smem = (char QIE_LDS*)smem_raw;
@@ -219,7 +230,10 @@ __global__ void __launch_bounds__(512) attn_pp_kernel(AttnArgs a) {
   auto mfma_i = [&](int i, const bf16x8_t& A) {
     if (i < 16) {
       const int cb = i >> 3, ks = i & 7;
-      if (ks == 0) mma32_z(st.s[cb], A, st.qf[0]);
+      if (ks == 0) {
+        if constexpr (PRE) mma32_c(st.s[cb], A, st.qf[0], st.negm);
+        else mma32_z(st.s[cb], A, st.qf[0]);
+      }
       else mma32(st.s[cb], A, st.qf[ks]);
     } else {
       const int j = i - 16;
@@ -271,7 +285,37 @@ __global__ void __launch_bounds__(512) attn_pp_kernel(AttnArgs a) {
 #pragma unroll
     for (int r = 0; r < 16; r += 2) { m0 = fmaxf(m0, st.s[1][r]); m1 = fmaxf(m1, st.s[1][r + 1]); }
     float mx = fmaxf(m0, m1);
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    {  // max with the partner half-wave (lane l <-> l ^ 32) without an LDS round trip
+      const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+      mx = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+    }
+    float ps0 = 0.f, ps1 = 0.f;
+    if constexpr (PRE) {
+      // S already holds s*c - m_run (log2 units)
+      if (__any(t == t0 || mx > kRescaleThr)) {
+        const float d = t == t0 ? mx : fmaxf(mx, 0.f);  // growth of the running max
+        const float alpha = __builtin_amdgcn_exp2f(-d);
+        st.m_run += d;
+        st.l_run *= alpha;
+#pragma unroll
+        for (int db = 0; db < 4; ++db) st.o[db] *= alpha;
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) st.s[cb] -= d;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) st.negm[r] = -st.m_run;
+      }
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+        for (int r = 0; r < 16; r += 2) {
+          const float p0 = __builtin_amdgcn_exp2f(st.s[cb][r]);
+          const float p1 = __builtin_amdgcn_exp2f(st.s[cb][r + 1]);
+          ps0 += p0;
+          ps1 += p1;
+          st.pf[cb * 2 + (r >> 3)][r & 7] = (__bf16)p0;
+          st.pf[cb * 2 + (r >> 3)][(r & 7) + 1] = (__bf16)p1;
+        }
+    } else {
     if (__any((mx - st.m_run) * c > kRescaleThr)) {
       const float m_new = fmaxf(st.m_run, mx);
       const float alpha = __builtin_amdgcn_exp2f((st.m_run - m_new) * c);
@@ -281,7 +325,6 @@ __global__ void __launch_bounds__(512) attn_pp_kernel(AttnArgs a) {
       for (int db = 0; db < 4; ++db) st.o[db] *= alpha;
     }
     const float mc = st.m_run * c;
-    float ps0 = 0.f, ps1 = 0.f;
 #pragma unroll
     for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
@@ -298,11 +341,13 @@ __global__ void __launch_bounds__(512) attn_pp_kernel(AttnArgs a) {
         st.pf[cb * 2 + (r >> 3)][r & 7] = (__bf16)p0;
         st.pf[cb * 2 + (r >> 3)][(r & 7) + 1] = (__bf16)p1;
       }
+    }
     st.l_run += ps0 + ps1;
 #pragma unroll
     for (int k = 0; k < 4; ++k) rfence(st.pf[k]);
     rfence(st.l_run);  // keep the row-sum adds in this phase (hipcc sinks them into the M-phase)
     rfence(st.m_run);
+    if constexpr (PRE) rfence(st.negm);
 #pragma unroll
     for (int db = 0; db < 4; ++db) rfence(st.o[db]);
     if (pieces == 4) asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
@@ -333,8 +378,9 @@ __global__ void __launch_bounds__(512) attn_pp_kernel(AttnArgs a) {
   if (grp == 1) asm volatile("s_barrier" ::: "memory");
 #pragma unroll
   for (int db = 0; db < 4; ++db) st.o[db] = f32x16_t{};
-  st.m_run = -INFINITY;
+  st.m_run = PRE ? 0.f : -INFINITY;  // PRE: finite (it is the MFMA's C); tile t0 sets it
   st.l_run = 0.f;
+  if constexpr (PRE) st.negm = f32x16_t{};
 
   auto mend = [&](int) { asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory"); };
   mphase(I0{}, I16{}, t0, t0);  // S(t0)
@@ -383,14 +429,19 @@ __global__ void __launch_bounds__(512) attn_pp_kernel(AttnArgs a) {
     dst = a.out_txt + ((int64_t)b * a.txt_rows + (s - a.s_img)) * (a.H * kDh) + h * kDh;
   }
   if (dst) {
+    // lane (ql, hf) holds d = 32db + 8g + 4hf + 0..3; one permlane32 swap per dword of the group
+    // pair (g, g+1) gives each lane 8 consecutive d (16-byte stores, T21)
 #pragma unroll
     for (int db = 0; db < 4; ++db)
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int d = 32 * db + 8 * g + 4 * hf;
-        const u32x2_t w = {pack2(st.o[db][4 * g] * inv, st.o[db][4 * g + 1] * inv),
-                           pack2(st.o[db][4 * g + 2] * inv, st.o[db][4 * g + 3] * inv)};
-        *(u32x2_t*)(dst + d) = w;
+      for (int g = 0; g < 4; g += 2) {
+        u32x2_t w0 = {pack2(st.o[db][4 * g] * inv, st.o[db][4 * g + 1] * inv),
+                      pack2(st.o[db][4 * g + 2] * inv, st.o[db][4 * g + 3] * inv)};
+        u32x2_t w1 = {pack2(st.o[db][4 * g + 4] * inv, st.o[db][4 * g + 5] * inv),
+                      pack2(st.o[db][4 * g + 6] * inv, st.o[db][4 * g + 7] * inv)};
+        const auto sx = __builtin_amdgcn_permlane32_swap(w0.x, w1.x, false, false);
+        const auto sy = __builtin_amdgcn_permlane32_swap(w0.y, w1.y, false, false);
+        *(u32x4_t*)(dst + 32 * db + 8 * g + 8 * hf) = u32x4_t{sx[0], sy[0], sx[1], sy[1]};
       }
   }
 }
@@ -457,14 +508,34 @@ int64_t split_bytes(int batch, int heads, int qblocks) {
 }
 }  // namespace
 
+namespace {
+// whole query blocks (+ the split tail and its combine when `ws` is given)
+int launch_attn(AttnArgs& a, bool pre, void* workspace, int64_t workspace_bytes, hipStream_t s) {
+  const int64_t need = workspace ? split_bytes(a.B, a.H, a.qblocks) : 0;
+  if (pre) a.c = 1.0f;  // logits already in log2 units (combine weights too)
+  if (need == 0) {      // no workspace, or a single query block: nothing to split
+    if (pre) attn_pp_kernel<true><<<a.qblocks * a.H * a.B, 512, 0, s>>>(a);
+    else attn_pp_kernel<false><<<a.qblocks * a.H * a.B, 512, 0, s>>>(a);
+    return qie_last_error();
+  }
+  QIE_CHECK_ARG(workspace_bytes >= need && ((uintptr_t)workspace % 16) == 0);
+  a.split = QIE_ATTN_SPLIT;
+  a.ws = (float*)workspace;
+  const int grid = ((a.qblocks - 1) + a.split) * a.H * a.B;
+  if (pre) attn_pp_kernel<true><<<grid, 512, 0, s>>>(a);
+  else attn_pp_kernel<false><<<grid, 512, 0, s>>>(a);
+  attn_combine_kernel<<<(a.B * a.H * kQB + 3) / 4, 256, 0, s>>>(a);
+  return qie_last_error();
+}
+}  // namespace
+
 extern "C" int qie_attention_fwd_bf16(const void* qkv, int batch, int heads, int s_pad,
                                       const int* kv_len_host, void* out_img, void* out_txt,
                                       int s_img, int txt_rows, float scale, qie_stream_t stream) {
   AttnArgs a;
   const int rc = attn_args(a, qkv, batch, heads, s_pad, kv_len_host, out_img, out_txt, s_img, txt_rows, scale);
   if (rc) return rc;
-  attn_pp_kernel<<<a.qblocks * heads * batch, 512, 0, (hipStream_t)stream>>>(a);
-  return qie_last_error();
+  return launch_attn(a, false, nullptr, 0, (hipStream_t)stream);
 }
 
 extern "C" int qie_attention_workspace_bytes(int batch, int heads, int s_pad, int s_img, int txt_rows,
@@ -481,17 +552,16 @@ extern "C" int qie_attention_fwd_split_bf16(const void* qkv, int batch, int head
   AttnArgs a;
   const int rc = attn_args(a, qkv, batch, heads, s_pad, kv_len_host, out_img, out_txt, s_img, txt_rows, scale);
   if (rc) return rc;
-  const int64_t need = split_bytes(batch, heads, a.qblocks);
-  const hipStream_t s = (hipStream_t)stream;
-  if (need == 0) {  // a single query block: nothing to split
-    attn_pp_kernel<<<a.qblocks * heads * batch, 512, 0, s>>>(a);
-    return qie_last_error();
-  }
-  QIE_CHECK_ARG(workspace && workspace_bytes >= need && ((uintptr_t)workspace % 16) == 0);
-  a.split = QIE_ATTN_SPLIT;
-  a.ws = (float*)workspace;
-  const int grid = ((a.qblocks - 1) + a.split) * heads * batch;
-  attn_pp_kernel<<<grid, 512, 0, s>>>(a);
-  attn_combine_kernel<<<(batch * heads * kQB + 3) / 4, 256, 0, s>>>(a);
-  return qie_last_error();
+  QIE_CHECK_ARG(workspace || split_bytes(batch, heads, a.qblocks) == 0);
+  return launch_attn(a, false, workspace, workspace_bytes, (hipStream_t)stream);
+}
+
+extern "C" int qie_attention_fwd_log2q_bf16(const void* qkv, int batch, int heads, int s_pad,
+                                            const int* kv_len_host, void* out_img, void* out_txt,
+                                            int s_img, int txt_rows, void* workspace,
+                                            int64_t workspace_bytes, qie_stream_t stream) {
+  AttnArgs a;
+  const int rc = attn_args(a, qkv, batch, heads, s_pad, kv_len_host, out_img, out_txt, s_img, txt_rows, 1.0f);
+  if (rc) return rc;
+  return launch_attn(a, true, workspace, workspace_bytes, (hipStream_t)stream);
 }

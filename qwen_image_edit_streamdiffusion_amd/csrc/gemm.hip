@@ -53,6 +53,7 @@ struct EpiArgs {
   const float* rcos;
   const float* rsin;
   float eps;
+  float qscale;  // EPI_QKV_NR: factor on q (1, or scale*log2(e) for qie_attention_fwd_log2q_bf16)
 };
 
 __device__ __forceinline__ int swz_chunk(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
@@ -495,6 +496,7 @@ __device__ __forceinline__ void ring_epilogue(typename MfmaOp<I8>::acc (&acc)[8]
 #pragma unroll
           for (int i = 0; i < 8; ++i) ss[i] = rsqrtf((ss[i] + red[(wave ^ 1) * 128 + i * 16 + fr]) * (1.0f / 128.0f) + e.eps);
           const bf16_t* nw = which == 0 ? e.nq : e.nk;
+          const float osc = which == 0 ? e.qscale : 1.0f;
           // pass 2: recompute the rounded values, RMSNorm (two bf16 roundings) and rotate
 #pragma unroll
           for (int jp = 0; jp < 2; ++jp) {
@@ -514,7 +516,7 @@ __device__ __forceinline__ void ring_epilogue(typename MfmaOp<I8>::acc (&acc)[8]
               for (int k = 0; k < 4; ++k) {
                 const float x0 = rbf(rbf(lo_f(w4[k]) * ss[i]) * lo_f(wv[k]));
                 const float x1 = rbf(rbf(hi_f(w4[k]) * ss[i]) * hi_f(wv[k]));
-                o[k] = pack2(x0 * cs[k] - x1 * sn[k], x0 * sn[k] + x1 * cs[k]);
+                o[k] = pack2((x0 * cs[k] - x1 * sn[k]) * osc, (x0 * sn[k] + x1 * cs[k]) * osc);
               }
               if (m < M) *(u32x4_t*)(row_ptr(m) + jp * 32) = u32x4_t{o[0], o[1], o[2], o[3]};
             }
@@ -1069,7 +1071,7 @@ int launch_splitk(const void* x, int64_t ldx, const void* w, int M, int N, int K
 template <bool I8>
 int launch_qkv_norm_rope(const void* x, int64_t ldx, const void* w, int M, int K, EpiArgs e,
                          const void* nq, const void* nk, const float* cos_tab, const float* sin_tab,
-                         float eps, hipStream_t s) {
+                         float eps, float q_scale, hipStream_t s) {
   QIE_CHECK_ARG(nq && nk && cos_tab && sin_tab && e.head_dim == 128);
   const int N = 3 * e.heads * e.head_dim;
   const int eb = I8 ? 1 : 2;
@@ -1086,6 +1088,7 @@ int launch_qkv_norm_rope(const void* x, int64_t ldx, const void* w, int M, int K
     e.rcos = cos_tab;
     e.rsin = sin_tab;
     e.eps = eps;
+    e.qscale = q_scale;
     gemm_pp_kernel<EPI_QKV_NR, I8><<<(int)big_tiles, 512, 0, s>>>((const char*)x, ldx * eb, (const char*)w,
                                                                  (int64_t)K * eb, M, N, K * eb, e);
     return qie_last_error();
@@ -1093,7 +1096,7 @@ int launch_qkv_norm_rope(const void* x, int64_t ldx, const void* w, int M, int K
   const int rc = launch_gemm<EPI_QKV, I8>(x, ldx, w, K, M, N, K, e, s);
   if (rc) return rc;
   return qie_qk_norm_rope_bf16(e.out, e.batch, e.heads, e.head_dim, e.s_pad, e.seq_offset, e.rows_per_batch,
-                               nq, nk, cos_tab, sin_tab, eps, s);
+                               nq, nk, cos_tab, sin_tab, eps, q_scale, s);
 }
 
 EpiArgs make_epi(void* out, int64_t ldo, const void* bias) {
@@ -1202,11 +1205,12 @@ extern "C" int qie_linear_qkv_norm_rope_bf16(const void* x, int64_t ldx, const v
                                              void* qkv, int M, int K, int rows_per_batch, int seq_offset,
                                              int batch, int heads, int head_dim, int s_pad, const void* wq,
                                              const void* wk, const float* cos_tab, const float* sin_tab,
-                                             float eps, qie_stream_t stream) {
+                                             float eps, float q_scale, qie_stream_t stream) {
   EpiArgs e = make_epi(qkv, 0, bias);
   int rc = qkv_args(e, M, rows_per_batch, seq_offset, batch, heads, head_dim, s_pad);
   if (rc) return rc;
-  return launch_qkv_norm_rope<false>(x, ldx, w, M, K, e, wq, wk, cos_tab, sin_tab, eps, (hipStream_t)stream);
+  return launch_qkv_norm_rope<false>(x, ldx, w, M, K, e, wq, wk, cos_tab, sin_tab, eps, q_scale,
+                                     (hipStream_t)stream);
 }
 
 extern "C" int qie_linear_qkv_norm_rope_i8(const void* xq, int64_t ldx, const float* sx, const void* wq,
@@ -1214,14 +1218,15 @@ extern "C" int qie_linear_qkv_norm_rope_i8(const void* xq, int64_t ldx, const fl
                                            int rows_per_batch, int seq_offset, int batch, int heads,
                                            int head_dim, int s_pad, const void* nq, const void* nk,
                                            const float* cos_tab, const float* sin_tab, float eps,
-                                           qie_stream_t stream) {
+                                           float q_scale, qie_stream_t stream) {
   QIE_CHECK_ARG(sx && sw);
   EpiArgs e = make_epi(qkv, 0, bias);
   e.sx = sx;
   e.sw = sw;
   int rc = qkv_args(e, M, rows_per_batch, seq_offset, batch, heads, head_dim, s_pad);
   if (rc) return rc;
-  return launch_qkv_norm_rope<true>(xq, ldx, wq, M, K, e, nq, nk, cos_tab, sin_tab, eps, (hipStream_t)stream);
+  return launch_qkv_norm_rope<true>(xq, ldx, wq, M, K, e, nq, nk, cos_tab, sin_tab, eps, q_scale,
+                                    (hipStream_t)stream);
 }
 
 // ---------------------------------------------------------------------------- split-K C ABI

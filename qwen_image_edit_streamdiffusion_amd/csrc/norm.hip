@@ -140,7 +140,7 @@ __global__ void __launch_bounds__(256)
     qk_norm_rope_kernel(bf16_t* __restrict__ qkv, int B, int H, int s_pad, int seg_start, int seg_len,
                         const bf16_t* __restrict__ wq, const bf16_t* __restrict__ wk,
                         const float* __restrict__ cos_tab, const float* __restrict__ sin_tab,
-                        float eps) {
+                        float eps, float q_scale) {
   const int64_t gr = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4);  // global row id
   const int64_t total = (int64_t)2 * B * H * seg_len;
   if (gr >= total) return;
@@ -160,13 +160,14 @@ __global__ void __launch_bounds__(256)
   unpack8(*(const u32x4_t*)((which == 0 ? wq : wk) + l16 * 8), w8);
   const f32x4_t cs = *(const f32x4_t*)(cos_tab + (int64_t)sl * 64 + l16 * 4);
   const f32x4_t sn = *(const f32x4_t*)(sin_tab + (int64_t)sl * 64 + l16 * 4);
+  const float osc = which == 0 ? q_scale : 1.0f;  // folded in before the one rounding of the output
   float o[8];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const float a = rbf(rbf(v[2 * j] * rstd) * w8[2 * j]);
     const float bb = rbf(rbf(v[2 * j + 1] * rstd) * w8[2 * j + 1]);
-    o[2 * j] = a * cs[j] - bb * sn[j];
-    o[2 * j + 1] = a * sn[j] + bb * cs[j];
+    o[2 * j] = (a * cs[j] - bb * sn[j]) * osc;
+    o[2 * j + 1] = (a * sn[j] + bb * cs[j]) * osc;
   }
   *(u32x4_t*)p = pack8(o);
 }
@@ -246,7 +247,7 @@ extern "C" int qie_rmsnorm_bf16(const void* x, const void* w, void* y, int rows,
 extern "C" int qie_qk_norm_rope_bf16(void* qkv, int batch, int heads, int head_dim, int s_pad,
                                      int seg_start, int seg_len, const void* wq, const void* wk,
                                      const float* cos_tab, const float* sin_tab, float eps,
-                                     qie_stream_t stream) {
+                                     float q_scale, qie_stream_t stream) {
   QIE_CHECK_ARG(qkv && wq && wk && cos_tab && sin_tab && head_dim == 128);
   QIE_CHECK_ARG(batch > 0 && heads > 0 && seg_len >= 0 && seg_start >= 0 &&
                 seg_start + seg_len <= s_pad);
@@ -256,7 +257,7 @@ extern "C" int qie_qk_norm_rope_bf16(void* qkv, int batch, int heads, int head_d
   QIE_CHECK_ARG(blocks < (1ll << 31));
   qk_norm_rope_kernel<<<(unsigned)blocks, 256, 0, (hipStream_t)stream>>>(
       (bf16_t*)qkv, batch, heads, s_pad, seg_start, seg_len, (const bf16_t*)wq, (const bf16_t*)wk,
-      cos_tab, sin_tab, eps);
+      cos_tab, sin_tab, eps, q_scale);
   return qie_last_error();
 }
 

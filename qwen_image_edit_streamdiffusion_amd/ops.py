@@ -118,7 +118,8 @@ def _rope_chk(qkv, rows_per_batch, wq, wk, cos_tab, sin_tab):
 
 def linear_qkv_norm_rope(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, qkv: torch.Tensor,
                          rows_per_batch: int, seq_offset: int, wq: torch.Tensor, wk: torch.Tensor,
-                         cos_tab: torch.Tensor, sin_tab: torch.Tensor, eps: float = 1e-6) -> None:
+                         cos_tab: torch.Tensor, sin_tab: torch.Tensor, eps: float = 1e-6,
+                         q_scale: float = 1.0) -> None:
     """linear_qkv followed by qk_norm_rope on the same rows, fused into the GEMM epilogue
     where the shape allows (qie_linear_qkv_norm_rope_bf16)."""
     _dev(x, w, b, qkv)
@@ -129,7 +130,7 @@ def linear_qkv_norm_rope(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, qkv:
     _chk(K % 64 == 0 and _is2d_rowmajor(x), "qkv K")
     _rope_chk(qkv, rows_per_batch, wq, wk, cos_tab, sin_tab)
     _lib.call("qie_linear_qkv_norm_rope_bf16", _p(x), x.stride(0), _p(w), _p(b), _p(qkv), M, K, rows_per_batch,
-              seq_offset, B, H, Dh, S_pad, _p(wq), _p(wk), _p(cos_tab), _p(sin_tab), eps, _stream())
+              seq_offset, B, H, Dh, S_pad, _p(wq), _p(wk), _p(cos_tab), _p(sin_tab), eps, q_scale, _stream())
 
 
 # ---------------------------------------------------------------------------- norms
@@ -169,7 +170,9 @@ def rmsnorm(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None
 
 
 def qk_norm_rope(qkv: torch.Tensor, seg_start: int, seg_len: int, wq: torch.Tensor, wk: torch.Tensor,
-                 cos_tab: torch.Tensor, sin_tab: torch.Tensor, eps: float = 1e-6):
+                 cos_tab: torch.Tensor, sin_tab: torch.Tensor, eps: float = 1e-6, q_scale: float = 1.0):
+    """Per-head RMSNorm + RoPE of the q and k rows of one segment, in place; q rows are also
+    multiplied by ``q_scale`` before their rounding (LOG2Q_SCALE feeds attention(log2q=True))."""
     _dev(qkv, wq, wk, cos_tab, sin_tab)
     _, B, H, S_pad, Dh = qkv.shape
     _chk(Dh == 128 and seg_start + seg_len <= S_pad, "qk_norm_rope segment")
@@ -177,7 +180,7 @@ def qk_norm_rope(qkv: torch.Tensor, seg_start: int, seg_len: int, wq: torch.Tens
          "rope table [seg_len, 64] fp32")
     _chk(cos_tab.is_contiguous() and sin_tab.is_contiguous() and sin_tab.shape == cos_tab.shape, "rope")
     _lib.call("qie_qk_norm_rope_bf16", _p(qkv), B, H, Dh, S_pad, seg_start, seg_len, _p(wq), _p(wk),
-              _p(cos_tab), _p(sin_tab), eps, _stream())
+              _p(cos_tab), _p(sin_tab), eps, q_scale, _stream())
 
 
 def quantize_rows(x: torch.Tensor, q: torch.Tensor, scale: torch.Tensor):
@@ -188,6 +191,8 @@ def quantize_rows(x: torch.Tensor, q: torch.Tensor, scale: torch.Tensor):
 
 
 # ---------------------------------------------------------------------------- attention
+LOG2Q_SCALE = 1.4426950408889634 / math.sqrt(128)  # q_scale for attention(log2q=True), head_dim 128
+
 def attention_workspace_bytes(B: int, H: int, S_pad: int, s_img: int, txt_rows: int) -> int:
     """Bytes of the split-key workspace ``attention(..., workspace=)`` uses (0: no split)."""
     n = ctypes.c_int64(0)
@@ -197,9 +202,11 @@ def attention_workspace_bytes(B: int, H: int, S_pad: int, s_img: int, txt_rows: 
 
 def attention(qkv: torch.Tensor, kv_len: Sequence[int], out_img: torch.Tensor,
               out_txt: Optional[torch.Tensor], s_img: int, txt_rows: int,
-              scale: Optional[float] = None, workspace: Optional[torch.Tensor] = None) -> None:
+              scale: Optional[float] = None, workspace: Optional[torch.Tensor] = None,
+              log2q: bool = False) -> None:
     """Joint attention. With ``workspace`` (>= attention_workspace_bytes) the last query block
-    of every (b, h) is split over the key range (qie_attention_fwd_split_bf16)."""
+    of every (b, h) is split over the key range (qie_attention_fwd_split_bf16). ``log2q``: the q
+    plane already holds q * scale * log2(e) (producers' ``q_scale``; qie_attention_fwd_log2q_bf16)."""
     _dev(qkv, out_img, out_txt)
     _, B, H, S_pad, Dh = qkv.shape
     _chk(Dh == 128 and S_pad % 256 == 0 and len(kv_len) == B and B <= 16, "attention shapes")
@@ -208,12 +215,19 @@ def attention(qkv: torch.Tensor, kv_len: Sequence[int], out_img: torch.Tensor,
         _chk(out_txt is not None and out_txt.shape == (B * txt_rows, H * Dh), "out_txt")
     _chk(all(0 < k <= S_pad for k in kv_len), "kv_len")
     arr = (ctypes.c_int * B)(*[int(k) for k in kv_len])
+    if workspace is not None:
+        _dev(workspace)
+    if log2q:
+        _chk(scale is None, "log2q: the scale is folded into q")
+        _lib.call("qie_attention_fwd_log2q_bf16", _p(qkv), B, H, S_pad, arr, _p(out_img), _p(out_txt), s_img,
+                  txt_rows, _p(workspace), 0 if workspace is None else workspace.numel() * workspace.element_size(),
+                  _stream())
+        return
     sc = 1.0 / math.sqrt(Dh) if scale is None else scale
     if workspace is None:
         _lib.call("qie_attention_fwd_bf16", _p(qkv), B, H, S_pad, arr, _p(out_img), _p(out_txt), s_img,
                   txt_rows, sc, _stream())
     else:
-        _dev(workspace)
         _lib.call("qie_attention_fwd_split_bf16", _p(qkv), B, H, S_pad, arr, _p(out_img), _p(out_txt),
                   s_img, txt_rows, sc, _p(workspace), workspace.numel() * workspace.element_size(), _stream())
 
@@ -336,7 +350,7 @@ def linear_qkv_i8(xq, sx, wq, sw, b, qkv, rows_per_batch: int, seq_offset: int):
 
 
 def linear_qkv_norm_rope_i8(xq, sx, wq8, sw, b, qkv, rows_per_batch: int, seq_offset: int, wq, wk,
-                            cos_tab, sin_tab, eps: float = 1e-6):
+                            cos_tab, sin_tab, eps: float = 1e-6, q_scale: float = 1.0):
     M, K = xq.shape
     _, B, H, S_pad, Dh = qkv.shape
     _chk(xq.dtype == torch.int8 and wq8.shape == (3 * H * Dh, K) and K % 128 == 0, "i8 qkv")
@@ -344,7 +358,7 @@ def linear_qkv_norm_rope_i8(xq, sx, wq8, sw, b, qkv, rows_per_batch: int, seq_of
     _rope_chk(qkv, rows_per_batch, wq, wk, cos_tab, sin_tab)
     _lib.call("qie_linear_qkv_norm_rope_i8", _p(xq), xq.stride(0), _p(sx), _p(wq8), _p(sw), _p(b), _p(qkv), M,
               K, rows_per_batch, seq_offset, B, H, Dh, S_pad, _p(wq), _p(wk), _p(cos_tab), _p(sin_tab), eps,
-              _stream())
+              q_scale, _stream())
 
 
 # ---------------------------------------------------------------------------- split-K linears

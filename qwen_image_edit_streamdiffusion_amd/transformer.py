@@ -184,6 +184,10 @@ class QwenImageTransformer2DModel(nn.Module):
         # image-stream QKV projection with the QK RMSNorm + RoPE in its epilogue (one launch);
         # False: the GEMM, then qie_qk_norm_rope_bf16 (A/B switch)
         self.fuse_qk_norm_rope = True
+        # q is written pre-multiplied by scale*log2(e) (q_scale of the QK-norm producers, before
+        # their one bf16 rounding) and the attention takes log2-unit logits straight from the
+        # MFMA (qie_attention_fwd_log2q_bf16); False: plain q, scale inside (A/B switch)
+        self.log2q_attention = True
         # K % 64 requirement of the GEMM kernels for the small input projections
         if in_channels % 64 or joint_attention_dim % 64:
             raise NotImplementedError("in_channels and joint_attention_dim must be multiples of 64")
@@ -512,7 +516,7 @@ class QwenImageTransformer2DModel(nn.Module):
         # ---- joint attention
         with self._probe("attention"):
             ops.attention(ws.qkv, kv_len, ws.att_img, ws.att_txt[:R_t] if has_txt else None, S_img, S_txt,
-                          workspace=ws.attn_split)
+                          workspace=ws.attn_split, log2q=self.log2q_attention)
         # ---- out-proj + gated residual, LN2 + modulate, MLP + gated residual
         if side is not None:
             side.wait_stream(main)
@@ -540,17 +544,18 @@ class QwenImageTransformer2DModel(nn.Module):
         else:
             ops.layernorm_modulate(x, m[:, 0:D], m[:, D:2 * D], rpb, out=h, eps=eps)
             inp = h
+        qs = ops.LOG2Q_SCALE if self.log2q_attention else 1.0
         if s == "img" and self.fuse_qk_norm_rope:  # one launch: GEMM + per-head RMSNorm + RoPE
             if self.int8:
                 wq8, sw = blk.q8["qkv_img"]
                 ops.linear_qkv_norm_rope_i8(qD, sc, wq8, sw, blk.b_qkv_img, ws.qkv, rpb, seq_off, nq, nk, cos,
-                                            sin, eps)
+                                            sin, eps, q_scale=qs)
             else:
                 ops.linear_qkv_norm_rope(h, blk.w_qkv_img, blk.b_qkv_img, ws.qkv, rpb, seq_off, nq, nk, cos,
-                                         sin, eps)
+                                         sin, eps, q_scale=qs)
             return
         self._linear(ws, blk, s, "qkv", inp, ops.EPI_QKV, ws.qkv, rpb=rpb, seq_off=seq_off)
-        ops.qk_norm_rope(ws.qkv, seq_off, rpb, nq, nk, cos, sin, eps)
+        ops.qk_norm_rope(ws.qkv, seq_off, rpb, nq, nk, cos, sin, eps, q_scale=qs)
 
     def _stream_post(self, blk: _Block, ws: _Workspace, st, eps):
         """x += gate1 (att W_out + b); h = LN2(x)(1 + scale2) + shift2;

@@ -50,7 +50,8 @@ def test_binding_table_matches_header(lib):
 
 
 def test_abi_version_and_strerror(lib):
-    assert lib.qie_abi_version() == 1
+    from qwen_image_edit_streamdiffusion_amd import _lib
+    assert lib.qie_abi_version() == _lib.ABI_VERSION == 2
     assert lib.qie_strerror(0) == b"ok"
     assert b"invalid" in lib.qie_strerror(-1)
 
@@ -65,12 +66,12 @@ def test_invalid_arguments_rejected_on_host(lib):
     assert lib.qie_attention_fwd_bf16(16, 1, 1, 300, kv, 16, 16, 256, 0, 0.1, None) == -1  # s_pad % 256
     dt = (ctypes.c_float * 1)(0.5)
     assert lib.qie_euler_step_bf16(16, 0, 16, 0, 16, 0, 17, 8, dt, None) == -1   # batch > 16
-    assert lib.qie_qk_norm_rope_bf16(16, 1, 1, 64, 256, 0, 8, 16, 16, 16, 16, 1e-6, None) == -1
+    assert lib.qie_qk_norm_rope_bf16(16, 1, 1, 64, 256, 0, 8, 16, 16, 16, 16, 1e-6, 1.0, None) == -1
     # fused QKV + QK-norm + RoPE: head_dim must be 128, norm/RoPE tables must be given
     assert lib.qie_linear_qkv_norm_rope_bf16(16, 256, 16, 16, 16, 512, 256, 256, 0, 2, 2, 64, 512,
-                                             16, 16, 16, 16, 1e-6, None) == -1
+                                             16, 16, 16, 16, 1e-6, 1.0, None) == -1
     assert lib.qie_linear_qkv_norm_rope_bf16(16, 256, 16, 16, 16, 512, 256, 256, 0, 2, 2, 128, 512,
-                                             None, 16, 16, 16, 1e-6, None) == -1
+                                             None, 16, 16, 16, 1e-6, 1.0, None) == -1
     with pytest.raises(_lib.QieError):
         _lib.call("qie_rmsnorm_bf16", None, None, None, 1, 8, 1e-6, None)
     # split-K: null epilogue, unknown kind, K not a multiple of splits * 64, workspace too small

@@ -45,6 +45,7 @@ def close(actual, ref, rel_l2=4e-3, ulps=2):
 
 
 RB = R._R(True)
+_R_F32 = R._R(False)  # no rounding: the kernel rounds the rotated (and q-scaled) value once
 
 
 @pytest.mark.parametrize("M,N,K", [(300, 384, 192), (2000, 2304, 128), (4300, 3072, 256),
@@ -132,7 +133,9 @@ def test_rmsnorm(dev, R_, D):
     close(ops.rmsnorm(x, w), R.rms_norm(x.cpu(), w.cpu(), 1e-6, RB))
 
 
-def test_qk_norm_rope(dev):
+@pytest.mark.parametrize("q_scale", [1.0, 1.4426950408889634 / math.sqrt(128)])
+def test_qk_norm_rope(dev, q_scale):
+    """q_scale multiplies the rotated q rows before their one rounding; k rows are unscaled."""
     ops = _ops()
     from qwen_image_edit_streamdiffusion_amd.rope import rope_tables
     B, H, s_pad = 2, 3, 512
@@ -142,13 +145,14 @@ def test_qk_norm_rope(dev):
     orig = qkv.clone()
     ws = [(1 + rnd((128,), dev, 0.1, 25 + i).float()).to(BF16) for i in range(4)]
     ic, is_, tc, ts = rope_tables(shapes, txt, dev)
-    ops.qk_norm_rope(qkv, 0, S_img, ws[0], ws[1], ic, is_)
-    ops.qk_norm_rope(qkv, S_img, txt, ws[2], ws[3], tc, ts)
+    ops.qk_norm_rope(qkv, 0, S_img, ws[0], ws[1], ic, is_, q_scale=q_scale)
+    ops.qk_norm_rope(qkv, S_img, txt, ws[2], ws[3], tc, ts, q_scale=q_scale)
     ip, tp = R.rope_phases(shapes, txt)
     for which in (0, 1):
         for seg, (a, n, wq, ph) in enumerate([(0, S_img, ws[which], ip), (S_img, txt, ws[2 + which], tp)]):
             x = orig[which, :, :, a:a + n].cpu().permute(0, 2, 1, 3)  # [B, S, H, Dh]
-            ref = R.apply_rope(R.rms_norm(x, wq.cpu(), 1e-6, RB), ph, RB).permute(0, 2, 1, 3)
+            ref = R.apply_rope(R.rms_norm(x, wq.cpu(), 1e-6, RB), ph, _R_F32).permute(0, 2, 1, 3)
+            ref = (ref * (q_scale if which == 0 else 1.0)).to(BF16)
             close(qkv[which, :, :, a:a + n], ref)
     assert torch.equal(qkv[2], orig[2])  # V untouched
     assert torch.equal(qkv[:, :, :, S_img + txt:], orig[:, :, :, S_img + txt:])
@@ -170,16 +174,17 @@ def _qkv_nr_case(dev, B, rpb, H, K, off, s_pad, seed, hw):
     (1, 4096, 16, 384, 0, 4352, (32, 64)),   # 16 x 24 tiles, K = 3 tiles
     (2, 200, 2, 128, 40, 512, (10, 10)),     # small: GEMM + qie_qk_norm_rope_bf16 fallback
 ])
-def test_qkv_norm_rope_fused(dev, B, rpb, H, K, off, s_pad, hw):
+@pytest.mark.parametrize("q_scale", [1.0, 0.12752])
+def test_qkv_norm_rope_fused(dev, B, rpb, H, K, off, s_pad, hw, q_scale):
     """QKV projection with QK RMSNorm + RoPE in the epilogue == the two-launch path (within the
     GEMM tolerance: only the fp32 order of the sum of squares differs) and the oracle."""
     ops = _ops()
     x, w, b, nq, nk, ic, is_, shapes = _qkv_nr_case(dev, B, rpb, H, K, off, s_pad, 70, hw)
     fused = torch.zeros(3, B, H, s_pad, 128, dtype=BF16, device=dev)
-    ops.linear_qkv_norm_rope(x, w, b, fused, rpb, off, nq, nk, ic, is_)
+    ops.linear_qkv_norm_rope(x, w, b, fused, rpb, off, nq, nk, ic, is_, q_scale=q_scale)
     two = torch.zeros_like(fused)
     ops.linear_qkv(x, w, b, two, rpb, off)
-    ops.qk_norm_rope(two, off, rpb, nq, nk, ic, is_)
+    ops.qk_norm_rope(two, off, rpb, nq, nk, ic, is_, q_scale=q_scale)
     sl = slice(off, off + rpb)
     close(fused[:, :, :, sl], two[:, :, :, sl])
     assert torch.equal(fused[2], two[2])  # V: no norm, same GEMM epilogue
@@ -187,7 +192,8 @@ def test_qkv_norm_rope_fused(dev, B, rpb, H, K, off, s_pad, hw):
     lin = R.linear(x.cpu(), w.cpu(), b.cpu(), RB).view(B, rpb, 3, H, 128)
     ip, _ = R.rope_phases(shapes, 16)
     for which, wn in ((0, nq), (1, nk)):
-        ref = R.apply_rope(R.rms_norm(lin[:, :, which], wn.cpu(), 1e-6, RB), ip, RB).permute(0, 2, 1, 3)
+        ref = R.apply_rope(R.rms_norm(lin[:, :, which], wn.cpu(), 1e-6, RB), ip, _R_F32).permute(0, 2, 1, 3)
+        ref = (ref * (q_scale if which == 0 else 1.0)).to(BF16)
         close(fused[which, :, :, sl], ref, rel_l2=8e-3, ulps=4)
 
 
@@ -201,22 +207,24 @@ def test_qkv_norm_rope_fused_i8(dev):
     sw = (torch.rand(3 * H * 128, generator=g) * 1e-3 + 1e-4).to(dev)
     _, _, b, nq, nk, ic, is_, _ = _qkv_nr_case(dev, B, rpb, H, K, 0, 2304, 73, (32, 32))
     fused = torch.zeros(3, B, H, 2304, 128, dtype=BF16, device=dev)
-    ops.linear_qkv_norm_rope_i8(xq, sx, wq8, sw, b, fused, rpb, 0, nq, nk, ic, is_)
+    ops.linear_qkv_norm_rope_i8(xq, sx, wq8, sw, b, fused, rpb, 0, nq, nk, ic, is_, q_scale=0.12752)
     two = torch.zeros_like(fused)
     ops.linear_qkv_i8(xq, sx, wq8, sw, b, two, rpb, 0)
-    ops.qk_norm_rope(two, 0, rpb, nq, nk, ic, is_)
+    ops.qk_norm_rope(two, 0, rpb, nq, nk, ic, is_, q_scale=0.12752)
     close(fused[:, :, :, :rpb], two[:, :, :, :rpb])
     assert torch.equal(fused[2], two[2])
 
 
-def _attn_ref(qkv, kv_len, s_img, txt_rows):
+def _attn_ref(qkv, kv_len, s_img, txt_rows, log2q=False):
+    """fp32 SDPA; log2q: the q plane holds q * scale * log2(e), i.e. logits in log2 units."""
     _, B, H, s_pad, Dh = qkv.shape
     S = s_img + txt_rows
     q, k, v = (qkv[i].float().cpu() for i in range(3))
+    sc = math.log(2.0) if log2q else 1.0 / math.sqrt(Dh)
     outs = []
     for b in range(B):
         L = kv_len[b]
-        s = q[b, :, :S] @ k[b, :, :L].transpose(-1, -2) / math.sqrt(Dh)
+        s = q[b, :, :S] @ k[b, :, :L].transpose(-1, -2) * sc
         o = torch.softmax(s, -1) @ v[b, :, :L]  # [H, S, Dh]
         outs.append(o.permute(1, 0, 2).reshape(S, H * Dh))
     o = torch.stack(outs)
@@ -291,6 +299,65 @@ def test_attention_spike_rescale(dev):
     oi = torch.empty(s_img, 128, dtype=BF16, device=dev)
     ops.attention(qkv, [s_img], oi, None, s_img, 0)
     ri, _ = _attn_ref(qkv, [s_img], s_img, 0)
+    close(oi, ri, rel_l2=1e-2, ulps=8)
+
+
+LOG2Q = 1.4426950408889634 / math.sqrt(128)
+
+
+@pytest.mark.parametrize("B,H,s_img,txt_rows,kv_len,qmul,split", [
+    (1, 2, 512, 40, [552], 1.0, True),
+    (2, 3, 1024, 216, [1240, 1100], 1.0, True),   # masked keys in row 1
+    (2, 2, 512, 40, [552, 530], 3.0, False),      # sharp softmax, rescales every few tiles
+    (1, 1, 256, 20, [100], 1.0, True),            # empty key ranges
+    (1, 1, 256, 0, [256], 1.0, True),             # one query block
+])
+def test_attention_log2q(dev, B, H, s_img, txt_rows, kv_len, qmul, split):
+    """qie_attention_fwd_log2q_bf16 on a q plane pre-multiplied by scale*log2(e) (one bf16
+    rounding of the product, as the producers' q_scale writes it) vs fp32 softmax in base 2,
+    and vs the plain kernel on the unscaled q."""
+    ops = _ops()
+    s_pad = ((s_img + txt_rows + 255) // 256) * 256
+    qkv = rnd((3, B, H, s_pad, 128), dev, 1.0, 36)
+    qkv[0] *= qmul
+    qkv[:, :, :, s_img + txt_rows:] = 0
+    pre = qkv.clone()
+    pre[0] = (qkv[0].float() * LOG2Q).to(BF16)
+    nb = ops.attention_workspace_bytes(B, H, s_pad, s_img, txt_rows)
+    ws = torch.full((max(nb // 4, 4),), float("nan"), device=dev) if split else None
+    oi = torch.empty(B * s_img, H * 128, dtype=BF16, device=dev)
+    ot = torch.empty(max(B * txt_rows, 1), H * 128, dtype=BF16, device=dev)
+    ops.attention(pre, kv_len, oi, ot[: B * txt_rows] if txt_rows else None, s_img, txt_rows,
+                  workspace=ws, log2q=True)
+    ri, rt = _attn_ref(pre, kv_len, s_img, txt_rows, log2q=True)
+    close(oi, ri, rel_l2=1e-2, ulps=8)
+    if txt_rows:
+        close(ot[: B * txt_rows], rt, rel_l2=1e-2, ulps=8)
+    oi2 = torch.empty_like(oi)
+    ot2 = torch.empty_like(ot)
+    ops.attention(qkv, kv_len, oi2, ot2[: B * txt_rows] if txt_rows else None, s_img, txt_rows, workspace=ws)
+    close(oi, oi2, rel_l2=1.5e-2, ulps=8)
+
+
+def test_attention_log2q_rescale_edges(dev):
+    """Query 0 sees only very negative logits (about -150 in log2 units: a running max clamped
+    at 0 would underflow every p to 0), query 3 a late spike, query 200 an early one: the
+    tile-t0 rescale must set the running max from the data."""
+    ops = _ops()
+    B, H, s_img = 1, 1, 512
+    qkv = rnd((3, B, H, s_img, 128), dev, 1.0, 37).float()
+    u = torch.randn(128, generator=torch.Generator().manual_seed(5)).to(dev)
+    qkv[1, 0, 0] += 3 * u                      # common key component
+    qkv[0, 0, 0, 0] = -3 * u                   # query 0 anti-aligned with every key
+    qkv[1, 0, 0, 450] = qkv[0, 0, 0, 3] * 6    # late spike for query 3
+    qkv[1, 0, 0, 5] = qkv[0, 0, 0, 200] * 6    # early spike for query 200
+    qkv = qkv.to(BF16)
+    pre = qkv.clone()
+    pre[0] = (qkv[0].float() * LOG2Q).to(BF16)
+    oi = torch.empty(s_img, 128, dtype=BF16, device=dev)
+    ops.attention(pre, [s_img], oi, None, s_img, 0, log2q=True)
+    ri, _ = _attn_ref(pre, [s_img], s_img, 0, log2q=True)
+    assert torch.isfinite(oi.float()).all()
     close(oi, ri, rel_l2=1e-2, ulps=8)
 
 

@@ -36,8 +36,11 @@ def load(path):
 
 def main():
     what = sys.argv[1]
-    paths = [a for a in sys.argv[2:] if a.endswith(".so")]
-    rest = [a for a in sys.argv[2:] if not a.endswith(".so")]
+    # "lib.so@log2q": the attention entry for a q plane pre-multiplied by scale*log2(e)
+    args = [a.split("@") for a in sys.argv[2:]]
+    paths = [a[0] for a in args if a[0].endswith(".so")]
+    modes = [a[1] if len(a) > 1 else "" for a in args if a[0].endswith(".so")]
+    rest = [a[0] for a in args if not a[0].endswith(".so")]
     rounds = int(rest[0]) if rest else 10
     libs = [load(p) for p in paths]
     dev = torch.device("cuda:0")
@@ -56,10 +59,18 @@ def main():
         flops = 4.0 * B * S * S * H * 128
 
         ws = torch.empty(B * H * 5 * 256 * 130, device=dev)  # QIE_ATTN_SPLIT = 5
+        qkv2 = qkv.clone()
+        qkv2[0] = (qkv[0].float() * (1.4426950408889634 / math.sqrt(128))).to(BF16)
 
         def run(i):
             lib = libs[i]
-            if what == "attention" and hasattr(lib, "qie_attention_fwd_split_bf16"):
+            if modes[i] == "log2q":
+                lib.qie_attention_fwd_log2q_bf16.argtypes = lib.qie_attention_fwd_bf16.argtypes[:-2] + [
+                    ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
+                rc = lib.qie_attention_fwd_log2q_bf16(
+                    qkv2.data_ptr(), B, H, s_pad, kv, outs[i][0].data_ptr(), outs[i][1].data_ptr(), S_IMG, S_TXT,
+                    ws.data_ptr() if what == "attention" else None, ws.numel() * 4, st)
+            elif what == "attention" and hasattr(lib, "qie_attention_fwd_split_bf16"):
                 rc = lib.qie_attention_fwd_split_bf16(qkv.data_ptr(), B, H, s_pad, kv, outs[i][0].data_ptr(),
                                                       outs[i][1].data_ptr(), S_IMG, S_TXT, 1 / math.sqrt(128),
                                                       ws.data_ptr(), ws.numel() * 4, st)
