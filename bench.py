@@ -103,6 +103,9 @@ def main():
                     help="A/B: image QKV GEMM and QK RMSNorm+RoPE as two launches")
     ap.add_argument("--no-log2q", action="store_true",
                     help="A/B: plain q and the softmax scale inside the attention (not log2-unit q)")
+    ap.add_argument("--text-splits", type=int, default=1,
+                    help="A/B: K ranges of the text-stream linears (1 = unsplit, the default; 0 = the "
+                         "latency-oriented split rule ops.splitk_splits)")
     ap.add_argument("--no-text-overlap", action="store_true",
                     help="A/B: run the text stream on the caller's stream, not on a second HIP stream")
     ap.add_argument("--force-dist", action="store_true",
@@ -132,6 +135,7 @@ def main():
     model.overlap_text_stream = not args.no_text_overlap
     model.fuse_qk_norm_rope = not args.no_qk_fusion
     model.log2q_attention = not args.no_log2q
+    model.text_splits = args.text_splits or None
     torch.cuda.synchronize()
     log(f"[bench] model built in {time.time() - t_build:.1f}s, "
         f"{torch.cuda.memory_allocated() / 1e9:.1f} GB")

@@ -238,7 +238,10 @@ int qie_linear_qkv_norm_rope_i8(const void* xq, int64_t ldx, const float* sx, co
  *   - workspace: caller-owned, >= splits * M * N * 4 bytes. Partials are fp32 for bf16 and
  *     int32 for int8, so the int8 result is bitwise the unsplit one.
  *   - The per-row arithmetic depends only on (K, splits), never on M, so rows stay batch
- *     independent (batched CFG == sequential). */
+ *     independent (batched CFG == sequential).
+ *   - splits == 1: one launch of 256x256 tiles with the epilogue applied directly (no partials,
+ *     no reduce; workspace may be NULL) -- the least CU-time per output, for launches that run
+ *     beside the image stream on a second HIP stream. */
 #define QIE_EPI_BIAS 0           /* y = bf16(x.W^T + b)                                        */
 #define QIE_EPI_GELU 1           /* y = gelu_tanh(bf16(x.W^T + b))                             */
 #define QIE_EPI_GATED_RESIDUAL 2 /* resid += bf16(gate[row/rows_per_batch] * bf16(x.W^T + b)) */

@@ -279,19 +279,36 @@ __global__ void __launch_bounds__(512) attn_pp_kernel(AttnArgs a) {
         }
     }
     const float c = a.c;
-    float m0 = fmaxf(st.s[0][0], st.s[0][1]), m1 = fmaxf(st.s[0][2], st.s[0][3]);
+    auto row_max = [&]() -> float {
+      float m0 = fmaxf(st.s[0][0], st.s[0][1]), m1 = fmaxf(st.s[0][2], st.s[0][3]);
 #pragma unroll
-    for (int r = 4; r < 16; r += 2) { m0 = fmaxf(m0, st.s[0][r]); m1 = fmaxf(m1, st.s[0][r + 1]); }
+      for (int r = 4; r < 16; r += 2) { m0 = fmaxf(m0, st.s[0][r]); m1 = fmaxf(m1, st.s[0][r + 1]); }
 #pragma unroll
-    for (int r = 0; r < 16; r += 2) { m0 = fmaxf(m0, st.s[1][r]); m1 = fmaxf(m1, st.s[1][r + 1]); }
-    float mx = fmaxf(m0, m1);
-    {  // max with the partner half-wave (lane l <-> l ^ 32) without an LDS round trip
-      const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
-      mx = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
-    }
+      for (int r = 0; r < 16; r += 2) { m0 = fmaxf(m0, st.s[1][r]); m1 = fmaxf(m1, st.s[1][r + 1]); }
+      const float mh = fmaxf(m0, m1);
+      // max with the partner half-wave (lane l <-> l ^ 32) without an LDS round trip
+      const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mh), __float_as_uint(mh), false, false);
+      return fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+    };
     float ps0 = 0.f, ps1 = 0.f;
+    auto exp_tile = [&]() {  // P = exp2(S), row sums, bf16 P^T fragments
+      ps0 = 0.f;
+      ps1 = 0.f;
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+        for (int r = 0; r < 16; r += 2) {
+          const float p0 = __builtin_amdgcn_exp2f(st.s[cb][r]);
+          const float p1 = __builtin_amdgcn_exp2f(st.s[cb][r + 1]);
+          ps0 += p0;
+          ps1 += p1;
+          st.pf[cb * 2 + (r >> 3)][r & 7] = (__bf16)p0;
+          st.pf[cb * 2 + (r >> 3)][(r & 7) + 1] = (__bf16)p1;
+        }
+    };
     if constexpr (PRE) {
-      // S already holds s*c - m_run (log2 units)
+      // S already holds s*c - m_run (log2 units); tile t0 always rescales (it sets m_run)
+      const float mx = row_max();
       if (__any(t == t0 || mx > kRescaleThr)) {
         const float d = t == t0 ? mx : fmaxf(mx, 0.f);  // growth of the running max
         const float alpha = __builtin_amdgcn_exp2f(-d);
@@ -304,18 +321,9 @@ __global__ void __launch_bounds__(512) attn_pp_kernel(AttnArgs a) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) st.negm[r] = -st.m_run;
       }
-#pragma unroll
-      for (int cb = 0; cb < 2; ++cb)
-#pragma unroll
-        for (int r = 0; r < 16; r += 2) {
-          const float p0 = __builtin_amdgcn_exp2f(st.s[cb][r]);
-          const float p1 = __builtin_amdgcn_exp2f(st.s[cb][r + 1]);
-          ps0 += p0;
-          ps1 += p1;
-          st.pf[cb * 2 + (r >> 3)][r & 7] = (__bf16)p0;
-          st.pf[cb * 2 + (r >> 3)][(r & 7) + 1] = (__bf16)p1;
-        }
+      exp_tile();
     } else {
+    const float mx = row_max();
     if (__any((mx - st.m_run) * c > kRescaleThr)) {
       const float m_new = fmaxf(st.m_run, mx);
       const float alpha = __builtin_amdgcn_exp2f((st.m_run - m_new) * c);

@@ -1037,12 +1037,34 @@ template <bool I8>
 int launch_splitk(const void* x, int64_t ldx, const void* w, int M, int N, int K, int splits,
                   int epi_kind, EpiArgs e, int64_t ws_bytes, hipStream_t s) {
   const int eb = I8 ? 1 : 2;
-  QIE_CHECK_ARG(x && w && e.out && e.bias && e.ws);
+  QIE_CHECK_ARG(x && w && e.out && e.bias);
   QIE_CHECK_ARG(M > 0 && N > 0 && K > 0 && N % 4 == 0 && splits >= 1 && splits <= 64);
   QIE_CHECK_ARG((K * eb) % (splits * kRowBytes) == 0);
   QIE_CHECK_ARG(((ldx * eb) % 16) == 0 && ((uintptr_t)x % 16) == 0 && ((uintptr_t)w % 16) == 0);
-  QIE_CHECK_ARG(((uintptr_t)e.ws % 16) == 0 && ws_bytes >= (int64_t)splits * M * N * 4);
   const int kb = K * eb / splits;
+  if (splits == 1) {
+    // one K range: the short-M tiles run with their real epilogue, no partials and no reduce
+    // (the least CU-time per output, which is what a side-stream launch costs its neighbours)
+    const bool wide = N % 8 == 0 && ((uintptr_t)e.out % 16) == 0 &&
+                      (epi_kind == EPI_QKV ? e.head_dim % 8 == 0 : e.ldo % 8 == 0) &&
+                      (epi_kind != EPI_GATE_RES || (((uintptr_t)e.gate % 16) == 0 && e.gate_bstride % 8 == 0));
+    if (QIE_GEMM_PP && wide && N >= 256 && kb >= 3 * kRowBytes) {
+      const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
+      const char* xc = (const char*)x;
+      const char* wc = (const char*)w;
+      const int64_t lx = ldx * eb, lw = (int64_t)K * eb;
+      switch (epi_kind) {
+        case EPI_BIAS: gemm_pp_kernel<EPI_BIAS, I8><<<tiles, 512, 0, s>>>(xc, lx, wc, lw, M, N, kb, e); break;
+        case EPI_GELU: gemm_pp_kernel<EPI_GELU, I8><<<tiles, 512, 0, s>>>(xc, lx, wc, lw, M, N, kb, e); break;
+        case EPI_GATE_RES:
+          gemm_pp_kernel<EPI_GATE_RES, I8><<<tiles, 512, 0, s>>>(xc, lx, wc, lw, M, N, kb, e);
+          break;
+        default: gemm_pp_kernel<EPI_QKV, I8><<<tiles, 512, 0, s>>>(xc, lx, wc, lw, M, N, kb, e); break;
+      }
+      return qie_last_error();
+    }
+  }
+  QIE_CHECK_ARG(e.ws && ((uintptr_t)e.ws % 16) == 0 && ws_bytes >= (int64_t)splits * M * N * 4);
   if (QIE_GEMM_PP && QIE_SPLITK_PP && M >= 128 && N >= 256 && kb >= 3 * kRowBytes) {
     // 256x256 ping-pong tiles (the text stream: M = B * S_txt ~ 432 -> 2 row tiles)
     const dim3 grid(((M + 255) / 256) * ((N + 255) / 256), splits);
@@ -1065,9 +1087,10 @@ int launch_splitk(const void* x, int64_t ldx, const void* w, int M, int N, int K
   return qie_last_error();
 }
 
-// QKV projection + QK RMSNorm + RoPE of one stream's rows: ONE gemm_pp launch (EPI_QKV_NR) when the
-// shape takes the big-tile path, otherwise the QKV GEMM followed by qie_qk_norm_rope_bf16 on the
-// same rows (the same arithmetic in two launches).
+// QKV projection + QK RMSNorm + RoPE of one stream's rows: ONE gemm_pp launch (EPI_QKV_NR) of
+// 256x256 tiles whenever K spans >= 3 tiles (also the text stream's 2 x 36 tiles: on
+// the side stream its CU-time, not its latency, is what it costs), otherwise the QKV GEMM followed
+// by qie_qk_norm_rope_bf16 on the same rows (the same arithmetic in two launches).
 template <bool I8>
 int launch_qkv_norm_rope(const void* x, int64_t ldx, const void* w, int M, int K, EpiArgs e,
                          const void* nq, const void* nk, const float* cos_tab, const float* sin_tab,
@@ -1076,7 +1099,9 @@ int launch_qkv_norm_rope(const void* x, int64_t ldx, const void* w, int M, int K
   const int N = 3 * e.heads * e.head_dim;
   const int eb = I8 ? 1 : 2;
   const int64_t big_tiles = (int64_t)((M + 255) / 256) * ((N + 255) / 256);
-  const bool fused = QIE_GEMM_PP && e.heads % 2 == 0 && M >= 256 && big_tiles >= 160 &&
+  // no condition on M: a row's arithmetic must not depend on the batch size (batched CFG ==
+  // sequential, stream batch == serial); rows past M are clamped / skipped by the kernel
+  const bool fused = QIE_GEMM_PP && e.heads % 2 == 0 &&
                      (int64_t)K * eb >= 3 * kRowBytes && ((int64_t)K * eb) % kRowBytes == 0 &&
                      ((ldx * eb) % 16) == 0 && ((uintptr_t)x % 16) == 0 && ((uintptr_t)w % 16) == 0 &&
                      ((uintptr_t)e.out % 16) == 0 && ((uintptr_t)nq % 16) == 0 && ((uintptr_t)nk % 16) == 0 &&

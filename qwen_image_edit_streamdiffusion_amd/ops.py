@@ -408,7 +408,8 @@ def linear_splitk(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, kind: int, 
     M, K = x.shape
     N = w.shape[0]
     _chk(_is2d_rowmajor(x) and w.shape[1] == K and b.numel() == N, "split-K shapes")
-    _chk(workspace.numel() * workspace.element_size() >= splitk_workspace_bytes(M, N, splits), "workspace")
+    _chk(splits == 1 or workspace.numel() * workspace.element_size() >= splitk_workspace_bytes(M, N, splits),
+         "workspace")
     e = _epilogue(kind, out, gate, rows_per_batch, seq_offset)
     _lib.call("qie_linear_splitk_bf16", _p(x), x.stride(0), _p(w), _p(b), ctypes.addressof(e), M, N, K,
               splits, _p(workspace), workspace.numel() * workspace.element_size(), _stream())
@@ -420,7 +421,8 @@ def linear_splitk_i8(xq, sx, wq, sw, b, kind: int, out: torch.Tensor, workspace:
     M, K = xq.shape
     N = wq.shape[0]
     _chk(xq.dtype == torch.int8 and wq.dtype == torch.int8 and wq.shape[1] == K, "i8 split-K")
-    _chk(workspace.numel() * workspace.element_size() >= splitk_workspace_bytes(M, N, splits), "workspace")
+    _chk(splits == 1 or workspace.numel() * workspace.element_size() >= splitk_workspace_bytes(M, N, splits),
+         "workspace")
     e = _epilogue(kind, out, gate, rows_per_batch, seq_offset)
     _lib.call("qie_linear_splitk_i8", _p(xq), xq.stride(0), _p(sx), _p(wq), _p(sw), _p(b),
               ctypes.addressof(e), M, N, K, splits, _p(workspace),

@@ -180,6 +180,10 @@ class QwenImageTransformer2DModel(nn.Module):
         # HIP stream beside the image stream; the two only meet at the joint attention (see
         # _block). False: everything on the caller's stream, in the same order (A/B switch).
         self.overlap_text_stream = True
+        # K ranges of the text-stream linears: None = ops.splitk_splits (latency-oriented), 1 =
+        # one launch of full-K tiles (least CU-time: the text launches share the chip with the
+        # image stream's, so what they cost is their CU-time, not their latency)
+        self.text_splits: Optional[int] = 1
         self._side: Optional[torch.cuda.Stream] = None
         # image-stream QKV projection with the QK RMSNorm + RoPE in its epilogue (one launch);
         # False: the GEMM, then qie_qk_norm_rope_bf16 (A/B switch)
@@ -545,14 +549,15 @@ class QwenImageTransformer2DModel(nn.Module):
             ops.layernorm_modulate(x, m[:, 0:D], m[:, D:2 * D], rpb, out=h, eps=eps)
             inp = h
         qs = ops.LOG2Q_SCALE if self.log2q_attention else 1.0
-        if s == "img" and self.fuse_qk_norm_rope:  # one launch: GEMM + per-head RMSNorm + RoPE
+        # one launch: GEMM + per-head RMSNorm + RoPE (the text stream too when its linears run unsplit)
+        if self.fuse_qk_norm_rope and (s == "img" or self.text_splits == 1):
             if self.int8:
-                wq8, sw = blk.q8["qkv_img"]
-                ops.linear_qkv_norm_rope_i8(qD, sc, wq8, sw, blk.b_qkv_img, ws.qkv, rpb, seq_off, nq, nk, cos,
-                                            sin, eps, q_scale=qs)
+                wq8, sw = blk.q8[f"qkv_{s}"]
+                ops.linear_qkv_norm_rope_i8(qD, sc, wq8, sw, getattr(blk, f"b_qkv_{s}"), ws.qkv, rpb, seq_off,
+                                            nq, nk, cos, sin, eps, q_scale=qs)
             else:
-                ops.linear_qkv_norm_rope(h, blk.w_qkv_img, blk.b_qkv_img, ws.qkv, rpb, seq_off, nq, nk, cos,
-                                         sin, eps, q_scale=qs)
+                ops.linear_qkv_norm_rope(h, getattr(blk, f"w_qkv_{s}"), getattr(blk, f"b_qkv_{s}"), ws.qkv, rpb,
+                                         seq_off, nq, nk, cos, sin, eps, q_scale=qs)
             return
         self._linear(ws, blk, s, "qkv", inp, ops.EPI_QKV, ws.qkv, rpb=rpb, seq_off=seq_off)
         ops.qk_norm_rope(ws.qkv, seq_off, rpb, nq, nk, cos, sin, eps, q_scale=qs)
@@ -590,7 +595,7 @@ class QwenImageTransformer2DModel(nn.Module):
         if isinstance(inp, tuple):
             (xq, sx), (wq, sw) = inp, blk.q8[f"{name}_{s}"]
             if s == "txt":
-                sp = ops.splitk_splits(wq.shape[0], wq.shape[1], int8=True)
+                sp = self.text_splits or ops.splitk_splits(wq.shape[0], wq.shape[1], int8=True)
                 return ops.linear_splitk_i8(xq, sx, wq, sw, b, kind, out, ws.splitk, sp, gate, rpb, seq_off)
             if kind == ops.EPI_QKV:
                 return ops.linear_qkv_i8(xq, sx, wq, sw, b, out, rpb, seq_off)
@@ -599,7 +604,7 @@ class QwenImageTransformer2DModel(nn.Module):
             return ops.linear_i8(xq, sx, wq, sw, b, out, act=ops.ACT_GELU if kind == ops.EPI_GELU else ops.ACT_NONE)
         w = getattr(blk, f"w_{name}_{s}")
         if s == "txt":
-            sp = ops.splitk_splits(w.shape[0], w.shape[1])
+            sp = self.text_splits or ops.splitk_splits(w.shape[0], w.shape[1])
             return ops.linear_splitk(inp, w, b, kind, out, ws.splitk, sp, gate, rpb, seq_off)
         if kind == ops.EPI_QKV:
             return ops.linear_qkv(inp, w, b, out, rpb, seq_off)

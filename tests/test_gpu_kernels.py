@@ -461,7 +461,8 @@ def test_linear_i8_gated_and_qkv(dev):
 
 # ------------------------------------------------------------------ split-K (text-stream) linears
 @pytest.mark.parametrize("M,N,K,splits", [(432, 3072, 3072, 4), (216, 3072, 12288, 8), (37, 512, 1024, 2),
-                                          (432, 1024, 768, 3), (130, 256, 512, 1)])
+                                          (432, 1024, 768, 3), (130, 256, 512, 1), (432, 3072, 3072, 1),
+                                          (37, 1024, 768, 1)])
 @pytest.mark.parametrize("kind", [0, 1, 2])
 def test_linear_splitk_vs_oracle(dev, M, N, K, splits, kind):
     """bf16 split-K: same tolerances as the unsplit GEMM (only the fp32 sum order differs)."""
@@ -483,7 +484,8 @@ def test_linear_splitk_vs_oracle(dev, M, N, K, splits, kind):
         close(y, R.gelu_tanh(lin, RB) if kind == ops.EPI_GELU else lin)
 
 
-def test_linear_splitk_qkv_matches_unsplit(dev):
+@pytest.mark.parametrize("splits", [4, 1])
+def test_linear_splitk_qkv_matches_unsplit(dev, splits):
     ops = _ops()
     B, H, Dh, rpb, s_pad, off, K = 2, 2, 128, 216, 512, 256, 3072
     x, w, b = rnd((B * rpb, K), dev, 1.0, 65), rnd((3 * H * Dh, K), dev, 0.02, 66), rnd((3 * H * Dh,), dev, 0.1, 67)
@@ -491,13 +493,14 @@ def test_linear_splitk_qkv_matches_unsplit(dev):
     c = torch.zeros_like(a)
     ops.linear_qkv(x, w, b, a, rpb, off)
     ws = torch.empty(ops.splitk_workspace_bytes(B * rpb, 3 * H * Dh, 4) // 4, device=dev)
-    ops.linear_splitk(x, w, b, ops.EPI_QKV, c, ws, 4, rows_per_batch=rpb, seq_offset=off)
+    ops.linear_splitk(x, w, b, ops.EPI_QKV, c, ws, splits, rows_per_batch=rpb, seq_offset=off)
     close(c[:, :, :, off:off + rpb], a[:, :, :, off:off + rpb])
     assert (c[:, :, :, :off] == 0).all() and (c[:, :, :, off + rpb:] == 0).all()
 
 
+@pytest.mark.parametrize("splits", [4, 1])
 @pytest.mark.parametrize("kind", [0, 1, 2, 3])
-def test_linear_splitk_i8_bitwise_equals_unsplit(dev, kind):
+def test_linear_splitk_i8_bitwise_equals_unsplit(dev, kind, splits):
     """int8 split-K sums int32 partials: bitwise the unsplit int8 result for every epilogue."""
     ops = _ops()
     g = torch.Generator().manual_seed(68)
@@ -513,16 +516,16 @@ def test_linear_splitk_i8_bitwise_equals_unsplit(dev, kind):
         a = torch.zeros(3, B, H, 512, 128, dtype=BF16, device=dev)
         c = torch.zeros_like(a)
         ops.linear_qkv_i8(xq, sx, wq, sw, b, a, rpb, 0)
-        ops.linear_splitk_i8(xq, sx, wq, sw, b, kind, c, ws, 4, rows_per_batch=rpb)
+        ops.linear_splitk_i8(xq, sx, wq, sw, b, kind, c, ws, splits, rows_per_batch=rpb)
     elif kind == ops.EPI_GATED_RESIDUAL:
         gate = rnd((B, N), dev, 0.5, 69)
         a = rnd((M, N), dev, 1.0, 70)
         c = a.clone()
         ops.linear_gated_residual_i8(xq, sx, wq, sw, b, gate, rpb, a)
-        ops.linear_splitk_i8(xq, sx, wq, sw, b, kind, c, ws, 4, gate=gate, rows_per_batch=rpb)
+        ops.linear_splitk_i8(xq, sx, wq, sw, b, kind, c, ws, splits, gate=gate, rows_per_batch=rpb)
     else:
         a = torch.empty(M, N, dtype=BF16, device=dev)
         c = torch.empty_like(a)
         ops.linear_i8(xq, sx, wq, sw, b, a, act=kind)
-        ops.linear_splitk_i8(xq, sx, wq, sw, b, kind, c, ws, 4)
+        ops.linear_splitk_i8(xq, sx, wq, sw, b, kind, c, ws, splits)
     assert torch.equal(a, c)
