@@ -269,6 +269,47 @@ int qie_linear_splitk_i8(const void* xq, int64_t ldx, const float* sx, const voi
                          int N, int K, int splits, void* workspace, int64_t workspace_bytes,
                          qie_stream_t stream);
 
+/* ------------------------------------------------------------------ VAE decoder (§8 f1)
+ * AutoencoderKLQwenImage.decode on one frame [U] (pipeline_qwenimage_edit_plus: unpack,
+ * `latents / (1/std) + mean`, vae.decode(z)[:, :, 0], postprocess). On a single frame every
+ * QwenImageCausalConv3d sees two zero frames of causal padding, so it is the 2-D convolution
+ * with the last temporal slice of its kernel; Resample "upsample3d" skips its time_conv on the
+ * first frame. Activations are NHWC bf16 [pixels][C]. */
+
+/* 3x3 (pad 1) or 1x1 convolution as an implicit GEMM: y[p][n] = bf16(sum_{tap,c} x[shift(p, tap)][c]
+ * * w[n][tap*C + c] + bias[n]) with the input gathered per tap (no im2col buffer); up = 1 folds a
+ * nearest-2x upsample into the gather (output H_in*2 x W_in*2). w: [N][ldw] bf16, K order
+ * [ky][kx][C], zero-padded to ldw >= roundup(ksize^2 * C, 64). resid != NULL (must equal y):
+ * y = bf16(y + bf16(acc + bias)) (ResidualBlock x + h). C % 8 == 0, N % 4 == 0. */
+int qie_conv2d_bf16(const void* x, int H_in, int W_in, int C, int up, int ksize, const void* w, int64_t ldw,
+                    const void* bias, const void* resid, void* y, int N, qie_stream_t stream);
+
+/* y[M][N] = x[M][K] . w[N][K]^T as raw fp32 (row strides ldx, ldw elements): attention scores of
+ * the VAE mid-block QwenImageAttentionBlock (one head over H*W tokens). K % 64 == 0. */
+int qie_matmul_f32out_bf16(const void* x, int64_t ldx, const void* w, int64_t ldw, float* y, int M, int N,
+                           int K, qie_stream_t stream);
+
+/* Packed latents [batch][(h/2)(w/2)][64] -> NHWC [batch][h][w][16]: _unpack_latents, then
+ * z = bf16(bf16(l / sinv[c]) + mean[c]) (sinv = bf16(1/std), mean bf16), then post_quant_conv
+ * y = bf16(pq_w[16][16] . z + pq_b). */
+int qie_vae_latents_in_bf16(const void* packed, int batch, int h, int w, const void* sinv, const void* mean,
+                            const void* pq_w, const void* pq_b, void* y, qie_stream_t stream);
+
+/* QwenImageRMS_norm over the C channels of each pixel (F.normalize * sqrt(C) * gamma, bf16
+ * rounding after each op), then SiLU when silu != 0. C % 8 == 0, C <= 512. */
+int qie_vae_rms_norm_bf16(const void* x, const void* gamma, void* y, int64_t pixels, int C, int silu,
+                          qie_stream_t stream);
+
+/* Row softmax of fp32 scores: p = bf16(exp(scale * (s - max)) / sum). N % 1024 == 0, N <= 16384. */
+int qie_softmax_rows_f32_bf16(const float* s, void* p, int rows, int N, float scale, qie_stream_t stream);
+
+/* y[c][r] = x[r][c] for an R x C bf16 block (row strides ldx, ldy elements). */
+int qie_transpose_bf16(const void* x, int64_t ldx, void* y, int64_t ldy, int R, int C, qie_stream_t stream);
+
+/* Decoder output [pixels][ldx] bf16 (channels 0..2) -> clamp(-1, 1) -> (x/2 + 0.5).clamp(0, 1)
+ * -> round(255 v) as uint8 RGB [pixels][3] (VaeImageProcessor.postprocess, output_type="pil"). */
+int qie_vae_rgb_out(const void* x, int64_t ldx, void* rgb, int64_t pixels, qie_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -64,6 +64,13 @@ SIGNATURES = {
     "qie_linear_qkv_norm_rope_i8": [P, L, P, P, P, P, P, I, I, I, I, I, I, I, I, P, P, P, P, F, F, P],
     "qie_linear_splitk_bf16": [P, L, P, P, P, I, I, I, I, P, L, P],
     "qie_linear_splitk_i8": [P, L, P, P, P, P, P, I, I, I, I, P, L, P],
+    "qie_conv2d_bf16": [P, I, I, I, I, I, P, L, P, P, P, I, P],
+    "qie_matmul_f32out_bf16": [P, L, P, L, P, I, I, I, P],
+    "qie_vae_latents_in_bf16": [P, I, I, I, P, P, P, P, P, P],
+    "qie_vae_rms_norm_bf16": [P, P, P, L, I, I, P],
+    "qie_softmax_rows_f32_bf16": [P, P, I, I, F, P],
+    "qie_transpose_bf16": [P, L, P, L, I, I, P],
+    "qie_vae_rgb_out": [P, L, P, L, P],
 }
 _RESTYPES = {"qie_strerror": c_char_p}
 

@@ -31,7 +31,8 @@ namespace {
 constexpr int kRowBytes = 128;  // one LDS tile row = 64 bf16 or 128 int8 of K
 
 // EPI_QKV_NR: EPI_QKV + the per-head RMSNorm of q and k and their RoPE (gemm_pp only)
-enum Epi { EPI_BIAS = 0, EPI_GELU = 1, EPI_GATE_RES = 2, EPI_QKV = 3, EPI_PARTIAL = 4, EPI_QKV_NR = 5 };
+// EPI_RES: out = bf16(out + bf16(acc + bias)) (the VAE ResidualBlock's x + h; conv_kernel only)
+enum Epi { EPI_BIAS = 0, EPI_GELU = 1, EPI_GATE_RES = 2, EPI_QKV = 3, EPI_PARTIAL = 4, EPI_QKV_NR = 5, EPI_RES = 6 };
 
 struct EpiArgs {
   void* out;          // y / resid / qkv base
@@ -127,6 +128,10 @@ __device__ __forceinline__ void epilogue4(const EpiArgs& e, int m, int n, const 
     }
     bf16_t* y = (bf16_t*)e.out + (int64_t)m * e.ldo + n;
     *(u32x2_t*)y = u32x2_t{pack2(v[0], v[1]), pack2(v[2], v[3])};
+  } else if constexpr (EPI == EPI_RES) {
+    bf16_t* x = (bf16_t*)e.out + (int64_t)m * e.ldo + n;
+    const u32x2_t xw = *(const u32x2_t*)x;
+    *(u32x2_t*)x = u32x2_t{pack2(lo_f(xw.x) + v[0], hi_f(xw.x) + v[1]), pack2(lo_f(xw.y) + v[2], hi_f(xw.y) + v[3])};
   } else if constexpr (EPI == EPI_GATE_RES) {
     const int b = m / e.rows_per_batch;
     const u32x2_t gw = *(const u32x2_t*)(e.gate + (int64_t)b * e.gate_bstride + n);
@@ -1124,6 +1129,143 @@ int launch_qkv_norm_rope(const void* x, int64_t ldx, const void* w, int M, int K
                                nq, nk, cos_tab, sin_tab, eps, q_scale, s);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Implicit-GEMM 3x3 / 1x1 convolution over NHWC bf16 activations (the VAE decoder's
+// QwenImageCausalConv3d on one frame and its Resample Conv2d): output pixel p
+// (row of the GEMM) x output channel (column), K = (tap, input channel) in [ky][kx][C] order,
+// zero padded to a multiple of 64. The X tile is gathered per lane straight from the input image
+// (one 16-byte chunk = 8 channels of one tap of one pixel per LDS-DMA lane): the shifted pixel of
+// the tap, through an optional nearest-2x upsample (source pixel = upsampled pixel >> 1), or the
+// zero chunk when the tap falls into the padding. No im2col buffer exists; W is [Cout][Kpad].
+// Body, LDS layout and epilogues are gemm_kernel<128, 128, 2, 2>'s.
+struct ConvArgs {
+  const bf16_t* in;
+  int H_in, W_in, C;    // input image (NHWC), C % 8 == 0
+  int H_out, W_out;     // output image; == input, or 2x with up
+  int up;               // 1: nearest-2x upsample folded into the gather
+  int ks;               // 3 (pad 1) or 1
+};
+__device__ __attribute__((aligned(16))) unsigned g_conv_zero[4];
+
+template <int EPI>
+__global__ void __launch_bounds__(256)
+    conv_kernel(ConvArgs c, const char* __restrict__ W, int64_t ldw_b, int M, int N, int K_bytes, EpiArgs e) {
+  using Op = MfmaOp<false>;
+  constexpr int BM = 128, BN = 128, WM = 2, WN = 2, NWAVE = 4;
+  constexpr int TM = BM / WM, TN = BN / WN, MT = TM / 16, NTL = TN / 16;
+  constexpr int A_BYTES = BM * kRowBytes, W_BYTES = BN * kRowBytes, STAGE = A_BYTES + W_BYTES;
+  constexpr int PX = BM / 8 / NWAVE;  // X pieces per lane per K tile
+  __shared__ __attribute__((aligned(16))) char smem_raw[2 * STAGE];
+  char QIE_LDS* smem = (char QIE_LDS*)smem_raw;
+
+  const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
+  const int nwg = tiles_m * tiles_n;
+  const int wgid = xcd_remap(blockIdx.x, nwg);
+  constexpr int GROUP = 8;
+  const int per_group = GROUP * tiles_n;
+  const int first_m = (wgid / per_group) * GROUP;
+  const int gsz = min(tiles_m - first_m, GROUP);
+  const int tm = first_m + (wgid % per_group) % gsz;
+  const int tn = (wgid % per_group) / gsz;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wm = wave / WN, wn = wave % WN;
+  const char* wg = W + (int64_t)n0 * ldw_b;
+  const int n_valid = N - n0;
+
+  // per X piece: output pixel (y, x) of its row, and the (tap, channel) of its chunk in the K tile
+  int py[PX], pxx[PX], tap[PX], ci[PX];
+  const int kreal = c.ks * c.ks * c.C;
+#pragma unroll
+  for (int i = 0; i < PX; ++i) {
+    const int r = (wave + i * NWAVE) * 8 + (lane >> 3);
+    const int p = min(m0 + r, M - 1);
+    py[i] = p / c.W_out;
+    pxx[i] = p - py[i] * c.W_out;
+    const int k = swz_chunk(r, lane & 7) * 8;  // K index of the chunk in tile 0
+    tap[i] = k / c.C;
+    ci[i] = k - tap[i] * c.C;
+  }
+  const char* zero = (const char*)g_conv_zero;
+  auto stage_x = [&](int kt, char QIE_LDS* lds) {
+#pragma unroll
+    for (int i = 0; i < PX; ++i) {
+      const char* src = zero;
+      if (tap[i] * c.C + ci[i] < kreal) {
+        int yy = py[i], xx = pxx[i];
+        if (c.ks == 3) {
+          const int dy = (tap[i] * 11) >> 5;  // tap / 3 for tap < 9
+          yy += dy - 1;
+          xx += tap[i] - 3 * dy - 1;
+        }
+        if (yy >= 0 && yy < c.H_out && xx >= 0 && xx < c.W_out) {
+          if (c.up) { yy >>= 1; xx >>= 1; }
+          src = (const char*)(c.in + ((int64_t)yy * c.W_in + xx) * c.C + ci[i]);
+        }
+      }
+      __builtin_amdgcn_global_load_lds((const void*)src, (QIE_LDS void*)(lds + (wave + i * NWAVE) * 1024), 16, 0, 0);
+      // advance to the next K tile: 64 channels on, wrapping into the following taps
+      ci[i] += 64;
+      while (ci[i] >= c.C) { ci[i] -= c.C; ++tap[i]; }
+    }
+  };
+
+  typename Op::acc acc[MT][NTL];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NTL; ++j) acc[i][j] = typename Op::acc{0, 0, 0, 0};
+
+  const int nk = K_bytes / kRowBytes;
+  stage_x(0, smem);
+  stage_tile<BN, NWAVE>(wg, ldw_b, n_valid, smem + A_BYTES, wave, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const int fr = lane & 15;
+  const int sw = (fr >> 1) & 7;
+  const int a_row = wm * TM + fr;
+  const int w_row = wn * TN + fr;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) {
+      char QIE_LDS* nb = smem + (cur ^ 1) * STAGE;
+      stage_x(kt + 1, nb);
+      stage_tile<BN, NWAVE>(wg + (int64_t)(kt + 1) * kRowBytes, ldw_b, n_valid, nb + A_BYTES, wave, lane);
+    }
+    const char QIE_LDS* at = smem + cur * STAGE;
+    const char QIE_LDS* wt = at + A_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int cofs = ((kk * 4 + (lane >> 4)) ^ sw) << 4;
+      typename Op::frag wf[NTL], af[MT];
+#pragma unroll
+      for (int j = 0; j < NTL; ++j) wf[j] = *(const typename Op::frag QIE_LDS*)(wt + (w_row + j * 16) * kRowBytes + cofs);
+#pragma unroll
+      for (int i = 0; i < MT; ++i) af[i] = *(const typename Op::frag QIE_LDS*)(at + (a_row + i * 16) * kRowBytes + cofs);
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NTL; ++j) acc[i][j] = Op::mma(wf[j], af[i], acc[i][j]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < MT; ++i) {
+    const int m = m0 + wm * TM + i * 16 + fr;
+    if (m >= M) continue;
+#pragma unroll
+    for (int j = 0; j < NTL; ++j) {
+      const int n = n0 + wn * TN + j * 16 + (lane >> 4) * 4;
+      if (n >= N) continue;
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r];
+      epilogue4<EPI, false>(e, m, n, v);
+    }
+  }
+}
+
 EpiArgs make_epi(void* out, int64_t ldo, const void* bias) {
   EpiArgs e{};
   e.out = out;
@@ -1301,4 +1443,55 @@ extern "C" int qie_linear_splitk_i8(const void* xq, int64_t ldx, const float* sx
   e.sw = sw;
   return launch_splitk<true>(xq, ldx, wq, M, N, K, splits, epi->kind, e, workspace_bytes,
                              (hipStream_t)stream);
+}
+
+// ---------------------------------------------------------------------------- VAE convolutions
+extern "C" int qie_conv2d_bf16(const void* x, int H_in, int W_in, int C, int up, int ksize, const void* w,
+                               int64_t ldw, const void* bias, const void* resid, void* y, int N,
+                               qie_stream_t stream) {
+  QIE_CHECK_ARG(x && w && bias && y && H_in > 0 && W_in > 0 && C > 0 && C % 8 == 0);
+  QIE_CHECK_ARG((up == 0 || up == 1) && (ksize == 1 || ksize == 3) && N > 0 && N % 4 == 0);
+  const int kreal = ksize * ksize * C;
+  const int kpad = (kreal + 63) / 64 * 64;
+  QIE_CHECK_ARG(ldw >= kpad && ldw % 8 == 0 && ((uintptr_t)w % 16) == 0 && ((uintptr_t)x % 16) == 0);
+  ConvArgs c{(const bf16_t*)x, H_in, W_in, C, H_in << up, W_in << up, up, ksize};
+  const int64_t M64 = (int64_t)c.H_out * c.W_out;
+  QIE_CHECK_ARG(M64 < (1ll << 31) && (int64_t)H_in * W_in * C < (1ll << 31));
+  const int M = (int)M64;
+  const int nwg = ((M + 127) / 128) * ((N + 127) / 128);
+  const hipStream_t s = (hipStream_t)stream;
+  if (resid) {  // y = bf16(resid + bf16(acc + bias)), in place on resid == y allowed
+    QIE_CHECK_ARG(resid == y);
+    EpiArgs e = make_epi(y, N, bias);
+    e.gate = nullptr;
+    e.rows_per_batch = M;
+    conv_kernel<EPI_RES><<<nwg, 256, 0, s>>>(c, (const char*)w, ldw * 2, M, N, kpad * 2, e);
+  } else {
+    EpiArgs e = make_epi(y, N, bias);
+    conv_kernel<EPI_BIAS><<<nwg, 256, 0, s>>>(c, (const char*)w, ldw * 2, M, N, kpad * 2, e);
+  }
+  return qie_last_error();
+}
+
+// Raw fp32 product y[M][N] = x[M][K] . w[N][K]^T (row strides ldx / ldw elements, no bias, no
+// rounding): the scores of the VAE mid-block attention (one head over H*W tokens).
+extern "C" int qie_matmul_f32out_bf16(const void* x, int64_t ldx, const void* w, int64_t ldw, float* y,
+                                      int M, int N, int K, qie_stream_t stream) {
+  QIE_CHECK_ARG(x && w && y && M > 0 && N > 0 && K > 0 && K % 64 == 0 && N % 4 == 0);
+  QIE_CHECK_ARG(ldx % 8 == 0 && ldw % 8 == 0 && ((uintptr_t)x % 16) == 0 && ((uintptr_t)w % 16) == 0);
+  QIE_CHECK_ARG(((uintptr_t)y % 16) == 0);
+  EpiArgs e = make_epi(y, N, nullptr);
+  e.ws = y;
+  const hipStream_t s = (hipStream_t)stream;
+  const int kb = K * 2;
+  if (QIE_GEMM_PP && M >= 256 && N >= 256 && kb >= 3 * kRowBytes) {
+    const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
+    gemm_pp_kernel<EPI_PARTIAL, false><<<tiles, 512, 0, s>>>((const char*)x, ldx * 2, (const char*)w, ldw * 2, M,
+                                                             N, kb, e);
+  } else {
+    const int nwg = ((M + 127) / 128) * ((N + 127) / 128);
+    gemm_kernel<128, 128, 2, 2, EPI_PARTIAL, false><<<nwg, 256, 0, s>>>((const char*)x, ldx * 2, (const char*)w,
+                                                                        ldw * 2, M, N, kb, e);
+  }
+  return qie_last_error();
 }

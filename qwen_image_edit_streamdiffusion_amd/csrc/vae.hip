@@ -1,0 +1,224 @@
+// VAE decoder (AutoencoderKLQwenImage on one frame) -- the memory-bound pieces
+// around the implicit-GEMM convolutions of gemm.hip (qie_conv2d_bf16). Activations are NHWC bf16
+// ([pixels][channels], channels contiguous), so every per-pixel channel reduction is one
+// contiguous row and every convolution is a GEMM over K = (tap, channel).
+//
+// Rounding points follow the bf16 module graph of diffusers' QwenImage VAE [U] (restated in
+// oracle/vae_ref.py): F.normalize (bf16 norm, bf16 quotient), * sqrt(C), * gamma, SiLU, each
+// rounded to bf16; the latent de-normalisation `latents / (1/std) + mean` in bf16.
+#include "qie_common.h"
+
+namespace {
+
+// ---- latents in: packed [B][(h/2)(w/2)][64] -> NHWC [B][h][w][16] (pipeline _unpack_latents),
+// z = bf16(bf16(l / sinv) + mean) per channel, then post_quant_conv (1x1x1, 16 -> 16, bias):
+// y[o] = bf16(sum_c W[o][c] z[c] + b[o]) in fp32. One thread per latent pixel.
+__global__ void __launch_bounds__(256)
+    latents_in_kernel(const bf16_t* __restrict__ packed, int B, int h, int w, const bf16_t* __restrict__ sinv,
+                      const bf16_t* __restrict__ mean, const bf16_t* __restrict__ W, const bf16_t* __restrict__ b,
+                      bf16_t* __restrict__ y) {
+  const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (p >= (int64_t)B * h * w) return;
+  const int bi = (int)(p / ((int64_t)h * w));
+  const int rem = (int)(p - (int64_t)bi * h * w);
+  const int yy = rem / w, xx = rem - yy * w;
+  const int i = yy >> 1, dy = yy & 1, j = xx >> 1, dx = xx & 1;
+  const bf16_t* src = packed + (((int64_t)bi * (h / 2) + i) * (w / 2) + j) * 64 + dy * 2 + dx;
+  float z[16];
+#pragma unroll
+  for (int c = 0; c < 16; ++c) z[c] = rbf(rbf(bf2f(src[c * 4]) / bf2f(sinv[c])) + bf2f(mean[c]));
+  u32x4_t o[2];
+  uint32_t* ow = (uint32_t*)o;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    float a[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int oc = 2 * q + t;
+      float acc = 0.f;
+#pragma unroll
+      for (int c = 0; c < 16; ++c) acc = __builtin_fmaf(bf2f(W[oc * 16 + c]), z[c], acc);
+      a[t] = acc + bf2f(b[oc]);
+    }
+    ow[q] = pack2(a[0], a[1]);
+  }
+  u32x4_t* dst = (u32x4_t*)(y + p * 16);
+  dst[0] = o[0];
+  dst[1] = o[1];
+}
+
+// ---- QwenImageRMS_norm (+ SiLU): per pixel, y = bf16(bf16(bf16(x / bf16(max(|x|_2, 1e-12))) *
+// sqrt(C)) * gamma), then optionally bf16(silu(y)). One wave per pixel, C <= 512, C % 8 == 0.
+template <bool SILU>
+__global__ void __launch_bounds__(256)
+    rms_norm_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ gamma, bf16_t* __restrict__ y,
+                    int64_t P, int C, float scale) {
+  const int64_t p = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (p >= P) return;
+  const int lane = threadIdx.x & 63;
+  const bf16_t* xr = x + p * C;
+  const bool act = lane * 8 < C;
+  u32x4_t raw = {0, 0, 0, 0};
+  if (act) raw = *(const u32x4_t*)(xr + lane * 8);
+  const uint32_t w4[4] = {raw.x, raw.y, raw.z, raw.w};
+  float v[8];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    v[2 * k] = lo_f(w4[k]);
+    v[2 * k + 1] = hi_f(w4[k]);
+  }
+  float ss = 0.f;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) ss = __builtin_fmaf(v[k], v[k], ss);
+  ss = wave_sum(ss);
+  const float d = fmaxf(rbf(sqrtf(ss)), 1e-12f);
+  if (!act) return;
+  u32x4_t graw = *(const u32x4_t*)(gamma + lane * 8);
+  const uint32_t g4[4] = {graw.x, graw.y, graw.z, graw.w};
+  uint32_t o[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    float r[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const float g = t ? hi_f(g4[k]) : lo_f(g4[k]);
+      float u = rbf(rbf(rbf(v[2 * k + t] / d) * scale) * g);
+      if (SILU) u = u / (1.0f + expf(-u));
+      r[t] = u;
+    }
+    o[k] = pack2(r[0], r[1]);
+  }
+  *(u32x4_t*)(y + p * C + lane * 8) = u32x4_t{o[0], o[1], o[2], o[3]};
+}
+
+// ---- softmax over rows of fp32 scores: P = bf16(exp(scale (s - max)) / sum), one workgroup per
+// row, N % 1024 == 0 and N <= 16384 (each thread keeps its N / 256 values in registers).
+template <int PER>
+__global__ void __launch_bounds__(256)
+    softmax_rows_kernel(const float* __restrict__ s, bf16_t* __restrict__ p, int N, float scale) {
+  const int64_t row = blockIdx.x;
+  const float* sr = s + row * N;
+  __shared__ float red[4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  float v[PER];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int q = 0; q < PER / 4; ++q) {
+    const f32x4_t t = *(const f32x4_t*)(sr + (q * 256 + tid) * 4);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      v[4 * q + k] = t[k];
+      mx = fmaxf(mx, t[k]);
+    }
+  }
+  mx = wave_max(mx);
+  if (lane == 0) red[wave] = mx;
+  __syncthreads();
+  mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  __syncthreads();
+  float sum = 0.f;
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    v[k] = __expf((v[k] - mx) * scale);
+    sum += v[k];
+  }
+  sum = wave_sum(sum);
+  if (lane == 0) red[wave] = sum;
+  __syncthreads();
+  const float inv = 1.0f / (red[0] + red[1] + red[2] + red[3]);
+  bf16_t* pr = p + row * N;
+#pragma unroll
+  for (int q = 0; q < PER / 4; ++q)
+    *(u32x2_t*)(pr + (q * 256 + tid) * 4) =
+        u32x2_t{pack2(v[4 * q] * inv, v[4 * q + 1] * inv), pack2(v[4 * q + 2] * inv, v[4 * q + 3] * inv)};
+}
+
+// ---- bf16 transpose: y[c][r] = x[r][c] for a [R][C] block with row stride ldx; 64x64 LDS tiles
+__global__ void __launch_bounds__(256)
+    transpose_kernel(const bf16_t* __restrict__ x, int64_t ldx, bf16_t* __restrict__ y, int64_t ldy, int R, int C) {
+  __shared__ bf16_t t[64][65];
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int i = ty; i < 64; i += 4) {
+    const int r = r0 + i, c = c0 + tx;
+    t[i][tx] = (r < R && c < C) ? x[(int64_t)r * ldx + c] : (bf16_t)0;
+  }
+  __syncthreads();
+  for (int i = ty; i < 64; i += 4) {
+    const int c = c0 + i, r = r0 + tx;
+    if (c < C && r < R) y[(int64_t)c * ldy + r] = t[tx][i];
+  }
+}
+
+// ---- image out: conv_out result [P][ldx] bf16 (channels 0..2) -> decode's clamp(-1, 1), then
+// the image processor's (x / 2 + 0.5).clamp(0, 1) on bf16 and (v * 255).round() -> uint8 RGB.
+__global__ void __launch_bounds__(256)
+    rgb_out_kernel(const bf16_t* __restrict__ x, int64_t ldx, uint8_t* __restrict__ rgb, int64_t P) {
+  const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (p >= P) return;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const float v = fminf(fmaxf(bf2f(x[p * ldx + c]), -1.0f), 1.0f);
+    const float u = fminf(fmaxf(rbf(v * 0.5f + 0.5f), 0.0f), 1.0f);
+    rgb[p * 3 + c] = (uint8_t)rintf(u * 255.0f);
+  }
+}
+
+}  // namespace
+
+extern "C" int qie_vae_latents_in_bf16(const void* packed, int batch, int h, int w, const void* sinv,
+                                       const void* mean, const void* pq_w, const void* pq_b, void* y,
+                                       qie_stream_t stream) {
+  QIE_CHECK_ARG(packed && sinv && mean && pq_w && pq_b && y && batch > 0 && h > 0 && w > 0);
+  QIE_CHECK_ARG(h % 2 == 0 && w % 2 == 0 && ((uintptr_t)y % 16) == 0);
+  const int64_t P = (int64_t)batch * h * w;
+  latents_in_kernel<<<(unsigned)((P + 255) / 256), 256, 0, (hipStream_t)stream>>>(
+      (const bf16_t*)packed, batch, h, w, (const bf16_t*)sinv, (const bf16_t*)mean, (const bf16_t*)pq_w,
+      (const bf16_t*)pq_b, (bf16_t*)y);
+  return qie_last_error();
+}
+
+extern "C" int qie_vae_rms_norm_bf16(const void* x, const void* gamma, void* y, int64_t pixels, int C,
+                                     int silu, qie_stream_t stream) {
+  QIE_CHECK_ARG(x && gamma && y && pixels > 0 && C > 0 && C % 8 == 0 && C <= 512);
+  QIE_CHECK_ARG(((uintptr_t)x % 16) == 0 && ((uintptr_t)y % 16) == 0 && ((uintptr_t)gamma % 16) == 0);
+  const unsigned grid = (unsigned)((pixels + 3) / 4);
+  const float scale = sqrtf((float)C);
+  if (silu)
+    rms_norm_kernel<true><<<grid, 256, 0, (hipStream_t)stream>>>((const bf16_t*)x, (const bf16_t*)gamma,
+                                                                 (bf16_t*)y, pixels, C, scale);
+  else
+    rms_norm_kernel<false><<<grid, 256, 0, (hipStream_t)stream>>>((const bf16_t*)x, (const bf16_t*)gamma,
+                                                                  (bf16_t*)y, pixels, C, scale);
+  return qie_last_error();
+}
+
+extern "C" int qie_softmax_rows_f32_bf16(const float* s, void* p, int rows, int N, float scale,
+                                         qie_stream_t stream) {
+  QIE_CHECK_ARG(s && p && rows > 0 && N > 0 && N % 1024 == 0 && N <= 16384);
+  const hipStream_t st = (hipStream_t)stream;
+  switch (N / 256) {
+    case 4: softmax_rows_kernel<4><<<rows, 256, 0, st>>>(s, (bf16_t*)p, N, scale); break;
+    case 8: softmax_rows_kernel<8><<<rows, 256, 0, st>>>(s, (bf16_t*)p, N, scale); break;
+    case 16: softmax_rows_kernel<16><<<rows, 256, 0, st>>>(s, (bf16_t*)p, N, scale); break;
+    case 32: softmax_rows_kernel<32><<<rows, 256, 0, st>>>(s, (bf16_t*)p, N, scale); break;
+    case 64: softmax_rows_kernel<64><<<rows, 256, 0, st>>>(s, (bf16_t*)p, N, scale); break;
+    default: return QIE_ERR_UNSUPPORTED;
+  }
+  return qie_last_error();
+}
+
+extern "C" int qie_transpose_bf16(const void* x, int64_t ldx, void* y, int64_t ldy, int R, int C,
+                                  qie_stream_t stream) {
+  QIE_CHECK_ARG(x && y && R > 0 && C > 0 && ldx >= C && ldy >= R);
+  const dim3 grid((C + 63) / 64, (R + 63) / 64);
+  transpose_kernel<<<grid, 256, 0, (hipStream_t)stream>>>((const bf16_t*)x, ldx, (bf16_t*)y, ldy, R, C);
+  return qie_last_error();
+}
+
+extern "C" int qie_vae_rgb_out(const void* x, int64_t ldx, void* rgb, int64_t pixels, qie_stream_t stream) {
+  QIE_CHECK_ARG(x && rgb && pixels > 0 && ldx >= 3);
+  rgb_out_kernel<<<(unsigned)((pixels + 255) / 256), 256, 0, (hipStream_t)stream>>>((const bf16_t*)x, ldx,
+                                                                                     (uint8_t*)rgb, pixels);
+  return qie_last_error();
+}

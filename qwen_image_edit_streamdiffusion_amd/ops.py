@@ -428,3 +428,104 @@ def linear_splitk_i8(xq, sx, wq, sw, b, kind: int, out: torch.Tensor, workspace:
               ctypes.addressof(e), M, N, K, splits, _p(workspace),
               workspace.numel() * workspace.element_size(), _stream())
     return out
+
+
+# ---------------------------------------------------------------------------- VAE decoder (§8 f1)
+def conv_kpad(C: int, ksize: int) -> int:
+    """Row length of a conv2d weight in the [Cout][ky][kx][C] layout qie_conv2d_bf16 reads."""
+    return -(-(ksize * ksize * C) // 64) * 64
+
+
+def conv2d(x: torch.Tensor, H: int, W: int, w: torch.Tensor, b: torch.Tensor, ksize: int = 3, up: bool = False,
+           out: Optional[torch.Tensor] = None, residual: bool = False) -> torch.Tensor:
+    """NHWC conv (pad ksize//2) as an implicit GEMM: x [H*W, C] -> [H'*W', N] with H' = 2H when
+    ``up`` (nearest-2x folded into the gather). w [N, conv_kpad(C, ksize)] bf16. ``residual``:
+    ``out`` holds the shortcut and receives bf16(out + bf16(conv + b))."""
+    _dev(x, w, b, out)
+    _chk(x.dtype == BF16 and w.dtype == BF16 and b.dtype == BF16, "bf16 operands required")
+    _chk(x.dim() == 2 and x.is_contiguous() and x.shape[0] == H * W, "x: [H*W, C] contiguous")
+    C = x.shape[1]
+    N = w.shape[0]
+    _chk(C % 8 == 0 and N % 4 == 0 and w.is_contiguous() and w.shape[1] >= conv_kpad(C, ksize), "conv shapes")
+    _chk(b.numel() == N, "bias")
+    P = H * W * (4 if up else 1)
+    if out is None:
+        _chk(not residual, "residual needs out")
+        out = torch.empty(P, N, dtype=BF16, device=x.device)
+    _chk(out.shape == (P, N) and out.is_contiguous() and out.dtype == BF16, "out [P, N]")
+    _lib.call("qie_conv2d_bf16", _p(x), H, W, C, int(up), ksize, _p(w), w.stride(0), _p(b),
+              _p(out) if residual else None, _p(out), N, _stream())
+    return out
+
+
+def matmul_f32out(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Raw fp32 x @ w.T for bf16 row-major views (row strides may exceed K)."""
+    _dev(x, w, out)
+    _chk(x.dtype == BF16 and w.dtype == BF16 and _is2d_rowmajor(x) and _is2d_rowmajor(w), "bf16 row-major")
+    M, K = x.shape
+    N = w.shape[0]
+    _chk(w.shape[1] == K and K % 64 == 0 and N % 4 == 0, "matmul shapes")
+    if out is None:
+        out = torch.empty(M, N, dtype=torch.float32, device=x.device)
+    _chk(out.shape == (M, N) and out.is_contiguous() and out.dtype == torch.float32, "out fp32 [M, N]")
+    _lib.call("qie_matmul_f32out_bf16", _p(x), x.stride(0), _p(w), w.stride(0), _p(out), M, N, K, _stream())
+    return out
+
+
+def softmax_rows(s: torch.Tensor, scale: float, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    _dev(s, out)
+    _chk(s.dtype == torch.float32 and s.dim() == 2 and s.is_contiguous(), "fp32 [rows, N]")
+    R, N = s.shape
+    if out is None:
+        out = torch.empty(R, N, dtype=BF16, device=s.device)
+    _chk(out.shape == (R, N) and out.is_contiguous() and out.dtype == BF16, "out")
+    _lib.call("qie_softmax_rows_f32_bf16", _p(s), _p(out), R, N, scale, _stream())
+    return out
+
+
+def transpose(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    _dev(x, out)
+    _chk(x.dtype == BF16 and _is2d_rowmajor(x), "bf16 row-major")
+    R, C = x.shape
+    if out is None:
+        out = torch.empty(C, R, dtype=BF16, device=x.device)
+    _chk(out.shape == (C, R) and _is2d_rowmajor(out), "out [C, R]")
+    _lib.call("qie_transpose_bf16", _p(x), x.stride(0), _p(out), out.stride(0), R, C, _stream())
+    return out
+
+
+def vae_latents_in(packed: torch.Tensor, h: int, w: int, sinv: torch.Tensor, mean: torch.Tensor,
+                   pq_w: torch.Tensor, pq_b: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Packed latents [B, (h/2)(w/2), 64] -> post_quant_conv(z) NHWC [B*h*w, 16]."""
+    _dev(packed, sinv, mean, pq_w, pq_b, out)
+    B = packed.shape[0]
+    _chk(packed.dtype == BF16 and packed.is_contiguous() and packed.shape[1:] == (h * w // 4, 64), "packed")
+    _chk(pq_w.shape == (16, 16) and pq_w.is_contiguous() and sinv.numel() == 16 and mean.numel() == 16, "consts")
+    if out is None:
+        out = torch.empty(B * h * w, 16, dtype=BF16, device=packed.device)
+    _chk(out.shape == (B * h * w, 16) and out.is_contiguous(), "out")
+    _lib.call("qie_vae_latents_in_bf16", _p(packed), B, h, w, _p(sinv), _p(mean), _p(pq_w), _p(pq_b), _p(out),
+              _stream())
+    return out
+
+
+def vae_rms_norm(x: torch.Tensor, gamma: torch.Tensor, silu: bool, out: Optional[torch.Tensor] = None):
+    """QwenImageRMS_norm over channels (+ SiLU) of NHWC [P, C]; out may be x (in place)."""
+    _dev(x, gamma, out)
+    _chk(x.dtype == BF16 and x.dim() == 2 and x.is_contiguous() and gamma.numel() == x.shape[1], "rms shapes")
+    if out is None:
+        out = torch.empty_like(x)
+    _chk(out.shape == x.shape and out.is_contiguous(), "out")
+    _lib.call("qie_vae_rms_norm_bf16", _p(x), _p(gamma), _p(out), x.shape[0], x.shape[1], int(silu), _stream())
+    return out
+
+
+def vae_rgb_out(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Decoder output [P, >=3] bf16 -> uint8 RGB [P, 3] (clamp, postprocess, round)."""
+    _dev(x, out)
+    _chk(x.dtype == BF16 and _is2d_rowmajor(x) and x.shape[1] >= 3, "x [P, >=3]")
+    if out is None:
+        out = torch.empty(x.shape[0], 3, dtype=torch.uint8, device=x.device)
+    _chk(out.shape == (x.shape[0], 3) and out.is_contiguous() and out.dtype == torch.uint8, "out")
+    _lib.call("qie_vae_rgb_out", _p(x), x.stride(0), _p(out), x.shape[0], _stream())
+    return out

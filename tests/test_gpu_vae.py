@@ -1,0 +1,165 @@
+"""VAE decoder on the GPU: every VAE entry point of libqie vs the CPU oracle
+(oracle/vae_ref.py, which keeps the causal 3-D form), then the whole decode.
+
+Tolerances (bf16 storage, fp32 accumulation):
+  * conv2d (implicit GEMM) vs fp32 F.conv2d on the same bf16 operands: rel-L2 <= 4e-3, max |diff|
+    <= 2 bf16 ulps of max|ref| (as the GEMMs); the residual form adds one more rounding: 4 ulps
+  * RMS_norm (+ SiLU), latents-in: rel-L2 <= 4e-3, 2 ulps (same rounding points as the oracle)
+  * softmax rows: rel-L2 <= 4e-3; transpose: exact; fp32 matmul: rel-L2 <= 1e-5
+  * whole decode (small config: base_dim 32, 32x32 latents -> 256x256): rel-L2 <= 3e-2 on the
+    [-1, 1] image (every conv/norm re-rounds to bf16), uint8 RGB: mean |diff| <= 1.5 levels
+"""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import vae_ref as V
+
+pytestmark = pytest.mark.gpu
+BF16 = torch.bfloat16
+
+
+def _ops():
+    from qwen_image_edit_streamdiffusion_amd import ops
+    return ops
+
+
+def rnd(shape, dev, scale=1.0, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.randn(shape, generator=g) * scale).to(BF16).to(dev)
+
+
+def close(actual, ref, rel_l2=4e-3, ulps=2):
+    a, r = actual.float().cpu(), ref.float().cpu()
+    assert a.shape == r.shape, (a.shape, r.shape)
+    assert torch.isfinite(a).all(), "non-finite output"
+    err = (a - r).norm() / max(r.norm().item(), 1e-30)
+    mx = (a - r).abs().max().item()
+    bound = ulps * 2.0 ** -8 * r.abs().max().item() + 1e-6
+    assert err <= rel_l2 and mx <= bound, f"rel_l2={err:.3e} max_abs={mx:.3e} bound={bound:.3e}"
+
+
+def _nhwc(x):  # [C, H, W] -> [H*W, C]
+    return x.permute(1, 2, 0).reshape(-1, x.shape[0]).contiguous()
+
+
+@pytest.mark.parametrize("H,W,C,N,k,up", [
+    (16, 16, 96, 96, 3, False),     # K = 864 -> padded 896
+    (32, 8, 16, 384, 3, False),     # conv_in shape: C = 16, K = 144 -> 192
+    (8, 16, 384, 192, 3, True),     # Resample: upsample folded into the gather
+    (16, 16, 192, 384, 1, False),   # conv_shortcut 1x1
+    (24, 20, 96, 4, 3, False),      # conv_out: 3 (+1 pad) channels, ragged tiles
+])
+def test_conv2d(dev, H, W, C, N, k, up):
+    from qwen_image_edit_streamdiffusion_amd.vae import conv_weight
+    ops = _ops()
+    x = rnd((C, H, W), dev, 1.0, 1)
+    w4 = rnd((N, C, k, k), dev, 1.0 / math.sqrt(C * k * k), 2)
+    b = rnd((N,), dev, 0.1, 3)
+    y = ops.conv2d(_nhwc(x), H, W, conv_weight(w4), b, ksize=k, up=up)
+    xi = x.float().cpu()[None]
+    if up:
+        xi = F.interpolate(xi, scale_factor=2.0, mode="nearest-exact")
+    ref = F.conv2d(xi, w4.float().cpu(), b.float().cpu(), padding=k // 2)[0].to(BF16)
+    close(y, _nhwc(ref))
+
+
+def test_conv2d_residual_and_causal3d(dev):
+    """A causal 3x3x3 conv on one frame (oracle: F.pad 2 zero frames + conv3d) == the 2-D conv with
+    the last temporal slice, and the residual epilogue adds onto the shortcut in place."""
+    from qwen_image_edit_streamdiffusion_amd.vae import conv_weight
+    ops = _ops()
+    H, W, C = 16, 24, 64
+    x = rnd((C, H, W), dev, 1.0, 4)
+    w5 = rnd((C, C, 3, 3, 3), dev, 1.0 / math.sqrt(27 * C), 5)
+    b = rnd((C,), dev, 0.1, 6)
+    h = rnd((C, H, W), dev, 1.0, 7)
+    r = V._R(True)
+    conv = V.causal_conv3d(x.float().cpu()[None, :, None], w5.cpu(), b.cpu(), 1, r)[0, :, 0]
+    ref = r(conv + h.float().cpu())
+    out = _nhwc(h)
+    ops.conv2d(_nhwc(x), H, W, conv_weight(w5), b, out=out, residual=True)
+    close(out, _nhwc(ref), ulps=4)
+
+
+@pytest.mark.parametrize("C,silu", [(96, True), (384, False), (192, True), (16, True)])
+def test_vae_rms_norm(dev, C, silu):
+    ops = _ops()
+    x = rnd((C, 8, 16), dev, 2.0, 8)
+    g = (1 + rnd((C,), dev, 0.1, 9).float()).to(BF16)
+    y = ops.vae_rms_norm(_nhwc(x), g, silu)
+    r = V._R(True)
+    ref = V.rms_norm(x.float().cpu()[None], g.cpu().view(C, 1, 1), r)
+    if silu:
+        ref = V.silu(ref, r)
+    close(y, _nhwc(ref[0]))
+    z = _nhwc(x)
+    ops.vae_rms_norm(z, g, silu, out=z)  # in place
+    assert torch.equal(z, y)
+
+
+def test_softmax_transpose_matmul(dev):
+    ops = _ops()
+    P, C = 2048, 384
+    qkv = rnd((P, 3 * C), dev, 1.0, 10)
+    q, k, v = qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:]
+    s = ops.matmul_f32out(q, k)
+    sref = q.float().cpu() @ k.float().cpu().T
+    assert ((s.cpu() - sref).norm() / sref.norm()).item() < 1e-5
+    p = ops.softmax_rows(s, 1.0 / math.sqrt(C))
+    close(p, torch.softmax(sref / math.sqrt(C), -1))
+    vt = ops.transpose(v)
+    assert torch.equal(vt.cpu(), v.cpu().T)
+
+
+def test_vae_latents_in(dev):
+    from qwen_image_edit_streamdiffusion_amd.vae import QwenImageVAEDecoder, VAEConfig
+    ops = _ops()
+    cfg = VAEConfig(base_dim=32)
+    dec = QwenImageVAEDecoder(cfg, dev).random_init_(3)
+    h, w = 16, 24
+    packed = rnd((2, h * w // 4, 64), dev, 1.0, 11)
+    y = ops.vae_latents_in(packed[1:].contiguous(), h, w, dec.w["sinv"], dec.w["mean"],
+                           dec.w["post_quant_conv.weight"], dec.w["post_quant_conv.bias"])
+    p = V.random_params(V.VAEConfig(base_dim=32), 3)
+    r = V._R(True)
+    z = V.unpack_latents(packed[1:].float().cpu(), h, w)
+    mean_t = torch.tensor(V.LATENTS_MEAN).view(1, -1, 1, 1, 1).to(BF16).float()
+    sinv = r(1.0 / torch.tensor(V.LATENTS_STD).view(1, -1, 1, 1, 1).to(BF16).float())
+    z = r(r(z / sinv) + mean_t)
+    ref = V.causal_conv3d(z, p["post_quant_conv.weight"], p["post_quant_conv.bias"], 0, r)[0, :, 0]
+    close(y, _nhwc(ref))
+
+
+def _small_decode(dev, seed=12):
+    from qwen_image_edit_streamdiffusion_amd.vae import QwenImageVAEDecoder, VAEConfig
+    cfg = VAEConfig(base_dim=32)
+    dec = QwenImageVAEDecoder(cfg, dev).random_init_(5)
+    h = w = 32  # mid-block attention over 1024 tokens; image 256 x 256
+    packed = rnd((1, h * w // 4, 64), dev, 1.0, seed)
+    p = V.random_params(V.VAEConfig(base_dim=32), 5)
+    return dec, packed, p, h, w
+
+
+def test_vae_decode_vs_oracle(dev):
+    dec, packed, p, h, w = _small_decode(dev)
+    img = dec.decode(packed, h, w, output="pt")[0]
+    ref = V.decode(p, packed.cpu(), h, w, V.VAEConfig(base_dim=32), emulate_bf16=True)[0]
+    assert img.shape == ref.shape == (3, 8 * h, 8 * w)
+    err = ((img.float().cpu() - ref).norm() / ref.norm()).item()
+    assert err <= 3e-2, err
+    u8 = dec.decode(packed, h, w)[0]
+    ru8 = V.to_uint8(ref[None])[0]
+    assert u8.shape == ru8.shape and u8.dtype == torch.uint8
+    assert (u8.cpu().float() - ru8.float()).abs().mean().item() <= 1.5
+
+
+def test_vae_decode_deterministic_and_batch_independent(dev):
+    dec, packed, _, h, w = _small_decode(dev, 13)
+    two = torch.cat([packed, rnd(packed.shape, dev, 1.0, 14)]).contiguous()
+    a = dec.decode(two, h, w)
+    b = dec.decode(packed, h, w)
+    assert torch.equal(a[:1], b)
+    assert torch.equal(dec.decode(packed, h, w), b)
