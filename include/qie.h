@@ -300,8 +300,10 @@ int qie_vae_latents_in_bf16(const void* packed, int batch, int h, int w, const v
 int qie_vae_rms_norm_bf16(const void* x, const void* gamma, void* y, int64_t pixels, int C, int silu,
                           qie_stream_t stream);
 
-/* Row softmax of fp32 scores: p = bf16(exp(scale * (s - max)) / sum). N % 1024 == 0, N <= 16384. */
-int qie_softmax_rows_f32_bf16(const float* s, void* p, int rows, int N, float scale, qie_stream_t stream);
+/* Row softmax of fp32 scores: p = bf16(exp(scale * (s - max)) / sum) for columns < N, zero in
+ * [N, ldp) (the K padding of the P.V GEMM). Row strides lds (floats), ldp (bf16); N % 4 == 0. */
+int qie_softmax_rows_f32_bf16(const float* s, int64_t lds, void* p, int64_t ldp, int rows, int N, float scale,
+                              qie_stream_t stream);
 
 /* y[c][r] = x[r][c] for an R x C bf16 block (row strides ldx, ldy elements). */
 int qie_transpose_bf16(const void* x, int64_t ldx, void* y, int64_t ldy, int R, int C, qie_stream_t stream);

@@ -68,7 +68,7 @@ SIGNATURES = {
     "qie_matmul_f32out_bf16": [P, L, P, L, P, I, I, I, P],
     "qie_vae_latents_in_bf16": [P, I, I, I, P, P, P, P, P, P],
     "qie_vae_rms_norm_bf16": [P, P, P, L, I, I, P],
-    "qie_softmax_rows_f32_bf16": [P, P, I, I, F, P],
+    "qie_softmax_rows_f32_bf16": [P, L, P, L, I, I, F, P],
     "qie_transpose_bf16": [P, L, P, L, I, I, P],
     "qie_vae_rgb_out": [P, L, P, L, P],
 }

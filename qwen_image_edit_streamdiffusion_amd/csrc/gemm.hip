@@ -1147,11 +1147,11 @@ struct ConvArgs {
 };
 __device__ __attribute__((aligned(16))) unsigned g_conv_zero[4];
 
-template <int EPI>
-__global__ void __launch_bounds__(256)
+template <int EPI, int BM, int WM>
+__global__ void __launch_bounds__(WM * 2 * 64)
     conv_kernel(ConvArgs c, const char* __restrict__ W, int64_t ldw_b, int M, int N, int K_bytes, EpiArgs e) {
   using Op = MfmaOp<false>;
-  constexpr int BM = 128, BN = 128, WM = 2, WN = 2, NWAVE = 4;
+  constexpr int BN = 128, WN = 2, NWAVE = WM * WN;
   constexpr int TM = BM / WM, TN = BN / WN, MT = TM / 16, NTL = TN / 16;
   constexpr int A_BYTES = BM * kRowBytes, W_BYTES = BN * kRowBytes, STAGE = A_BYTES + W_BYTES;
   constexpr int PX = BM / 8 / NWAVE;  // X pieces per lane per K tile
@@ -1458,17 +1458,20 @@ extern "C" int qie_conv2d_bf16(const void* x, int H_in, int W_in, int C, int up,
   const int64_t M64 = (int64_t)c.H_out * c.W_out;
   QIE_CHECK_ARG(M64 < (1ll << 31) && (int64_t)H_in * W_in * C < (1ll << 31));
   const int M = (int)M64;
-  const int nwg = ((M + 127) / 128) * ((N + 127) / 128);
   const hipStream_t s = (hipStream_t)stream;
-  if (resid) {  // y = bf16(resid + bf16(acc + bias)), in place on resid == y allowed
-    QIE_CHECK_ARG(resid == y);
-    EpiArgs e = make_epi(y, N, bias);
-    e.gate = nullptr;
-    e.rows_per_batch = M;
-    conv_kernel<EPI_RES><<<nwg, 256, 0, s>>>(c, (const char*)w, ldw * 2, M, N, kpad * 2, e);
+  QIE_CHECK_ARG(!resid || resid == y);  // y = bf16(resid + bf16(acc + bias)), in place
+  EpiArgs e = make_epi(y, N, bias);
+  const char* wc = (const char*)w;
+  // 256-pixel tiles (8 waves) once they still give >= 2 workgroups per CU, else 128 (4 waves)
+  const int tn = (N + 127) / 128;
+  const int64_t big = (int64_t)((M + 255) / 256) * tn;
+  if (big >= 512) {
+    if (resid) conv_kernel<EPI_RES, 256, 4><<<(int)big, 512, 0, s>>>(c, wc, ldw * 2, M, N, kpad * 2, e);
+    else conv_kernel<EPI_BIAS, 256, 4><<<(int)big, 512, 0, s>>>(c, wc, ldw * 2, M, N, kpad * 2, e);
   } else {
-    EpiArgs e = make_epi(y, N, bias);
-    conv_kernel<EPI_BIAS><<<nwg, 256, 0, s>>>(c, (const char*)w, ldw * 2, M, N, kpad * 2, e);
+    const int nwg = ((M + 127) / 128) * tn;
+    if (resid) conv_kernel<EPI_RES, 128, 2><<<nwg, 256, 0, s>>>(c, wc, ldw * 2, M, N, kpad * 2, e);
+    else conv_kernel<EPI_BIAS, 128, 2><<<nwg, 256, 0, s>>>(c, wc, ldw * 2, M, N, kpad * 2, e);
   }
   return qie_last_error();
 }

@@ -6,6 +6,8 @@
 // Rounding points follow the bf16 module graph of diffusers' QwenImage VAE [U] (restated in
 // oracle/vae_ref.py): F.normalize (bf16 norm, bf16 quotient), * sqrt(C), * gamma, SiLU, each
 // rounded to bf16; the latent de-normalisation `latents / (1/std) + mean` in bf16.
+#include <type_traits>
+
 #include "qie_common.h"
 
 namespace {
@@ -48,18 +50,18 @@ __global__ void __launch_bounds__(256)
 }
 
 // ---- QwenImageRMS_norm (+ SiLU): per pixel, y = bf16(bf16(bf16(x / bf16(max(|x|_2, 1e-12))) *
-// sqrt(C)) * gamma), then optionally bf16(silu(y)). One wave per pixel, C <= 512, C % 8 == 0.
-template <bool SILU>
+// sqrt(C)) * gamma), then optionally bf16(silu(y)). G lanes per pixel (8 channels, one 16-byte
+// load each; C <= 8 G), 64 / G pixels per wave: every lane of the wave moves bytes.
+template <bool SILU, int G>
 __global__ void __launch_bounds__(256)
     rms_norm_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ gamma, bf16_t* __restrict__ y,
                     int64_t P, int C, float scale) {
-  const int64_t p = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (p >= P) return;
-  const int lane = threadIdx.x & 63;
+  const int64_t p = ((int64_t)blockIdx.x * 256 + threadIdx.x) / G;
+  const int gl = threadIdx.x & (G - 1);
+  const bool act = p < P && gl * 8 < C;
   const bf16_t* xr = x + p * C;
-  const bool act = lane * 8 < C;
   u32x4_t raw = {0, 0, 0, 0};
-  if (act) raw = *(const u32x4_t*)(xr + lane * 8);
+  if (act) raw = *(const u32x4_t*)(xr + gl * 8);
   const uint32_t w4[4] = {raw.x, raw.y, raw.z, raw.w};
   float v[8];
 #pragma unroll
@@ -70,10 +72,10 @@ __global__ void __launch_bounds__(256)
   float ss = 0.f;
 #pragma unroll
   for (int k = 0; k < 8; ++k) ss = __builtin_fmaf(v[k], v[k], ss);
-  ss = wave_sum(ss);
+  ss = group_sum<G>(ss);
   const float d = fmaxf(rbf(sqrtf(ss)), 1e-12f);
   if (!act) return;
-  u32x4_t graw = *(const u32x4_t*)(gamma + lane * 8);
+  u32x4_t graw = *(const u32x4_t*)(gamma + gl * 8);
   const uint32_t g4[4] = {graw.x, graw.y, graw.z, graw.w};
   uint32_t o[4];
 #pragma unroll
@@ -83,54 +85,58 @@ __global__ void __launch_bounds__(256)
     for (int t = 0; t < 2; ++t) {
       const float g = t ? hi_f(g4[k]) : lo_f(g4[k]);
       float u = rbf(rbf(rbf(v[2 * k + t] / d) * scale) * g);
-      if (SILU) u = u / (1.0f + expf(-u));
+      if (SILU) u = u * __builtin_amdgcn_rcpf(1.0f + __expf(-u));
       r[t] = u;
     }
     o[k] = pack2(r[0], r[1]);
   }
-  *(u32x4_t*)(y + p * C + lane * 8) = u32x4_t{o[0], o[1], o[2], o[3]};
+  *(u32x4_t*)(y + p * C + gl * 8) = u32x4_t{o[0], o[1], o[2], o[3]};
 }
 
-// ---- softmax over rows of fp32 scores: P = bf16(exp(scale (s - max)) / sum), one workgroup per
-// row, N % 1024 == 0 and N <= 16384 (each thread keeps its N / 256 values in registers).
-template <int PER>
+// ---- softmax over rows of fp32 scores: P = bf16(exp(scale (s - max)) / sum) for columns < N,
+// zeros in [N, ldp) (the K padding of the P.V GEMM). One workgroup per row, N % 4 == 0: pass 1
+// keeps a per-thread online (max, sum) over its float4s, merged across the workgroup; pass 2
+// re-reads the row (L2-resident, <= 64 KiB) and writes P.
+__device__ __forceinline__ void ml_merge(float& m, float& l, float m2, float l2) {
+  const float mn = fmaxf(m, m2);
+  l = (m == -INFINITY ? 0.f : l * __expf(m - mn)) + (m2 == -INFINITY ? 0.f : l2 * __expf(m2 - mn));
+  m = mn;
+}
+
 __global__ void __launch_bounds__(256)
-    softmax_rows_kernel(const float* __restrict__ s, bf16_t* __restrict__ p, int N, float scale) {
+    softmax_rows_kernel(const float* __restrict__ s, int64_t lds, bf16_t* __restrict__ p, int64_t ldp, int N,
+                        float scale) {
   const int64_t row = blockIdx.x;
-  const float* sr = s + row * N;
-  __shared__ float red[4];
+  const float* sr = s + row * lds;
+  __shared__ float red_m[4], red_l[4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  float v[PER];
-  float mx = -INFINITY;
+  float m = -INFINITY, l = 0.f;  // in scaled units
+  for (int c = tid * 4; c < N; c += 1024) {
+    const f32x4_t t = *(const f32x4_t*)(sr + c);
+    const float tm = fmaxf(fmaxf(t[0], t[1]), fmaxf(t[2], t[3])) * scale;
+    float tl = 0.f;
 #pragma unroll
-  for (int q = 0; q < PER / 4; ++q) {
-    const f32x4_t t = *(const f32x4_t*)(sr + (q * 256 + tid) * 4);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      v[4 * q + k] = t[k];
-      mx = fmaxf(mx, t[k]);
-    }
+    for (int k = 0; k < 4; ++k) tl += __expf(t[k] * scale - tm);
+    ml_merge(m, l, tm, tl);
   }
-  mx = wave_max(mx);
-  if (lane == 0) red[wave] = mx;
-  __syncthreads();
-  mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-  __syncthreads();
-  float sum = 0.f;
 #pragma unroll
-  for (int k = 0; k < PER; ++k) {
-    v[k] = __expf((v[k] - mx) * scale);
-    sum += v[k];
+  for (int o = 32; o > 0; o >>= 1) ml_merge(m, l, __shfl_xor(m, o, 64), __shfl_xor(l, o, 64));
+  if (lane == 0) {
+    red_m[wave] = m;
+    red_l[wave] = l;
   }
-  sum = wave_sum(sum);
-  if (lane == 0) red[wave] = sum;
   __syncthreads();
-  const float inv = 1.0f / (red[0] + red[1] + red[2] + red[3]);
-  bf16_t* pr = p + row * N;
-#pragma unroll
-  for (int q = 0; q < PER / 4; ++q)
-    *(u32x2_t*)(pr + (q * 256 + tid) * 4) =
-        u32x2_t{pack2(v[4 * q] * inv, v[4 * q + 1] * inv), pack2(v[4 * q + 2] * inv, v[4 * q + 3] * inv)};
+  m = red_m[0];
+  l = red_l[0];
+  for (int w = 1; w < 4; ++w) ml_merge(m, l, red_m[w], red_l[w]);
+  const float inv = 1.0f / l;
+  bf16_t* pr = p + row * ldp;
+  for (int c = tid * 4; c < N; c += 1024) {
+    const f32x4_t t = *(const f32x4_t*)(sr + c);
+    *(u32x2_t*)(pr + c) = u32x2_t{pack2(__expf(t[0] * scale - m) * inv, __expf(t[1] * scale - m) * inv),
+                                  pack2(__expf(t[2] * scale - m) * inv, __expf(t[3] * scale - m) * inv)};
+  }
+  for (int c = N + tid * 4; c < ldp; c += 1024) *(u32x2_t*)(pr + c) = u32x2_t{0u, 0u};
 }
 
 // ---- bf16 transpose: y[c][r] = x[r][c] for a [R][C] block with row stride ldx; 64x64 LDS tiles
@@ -182,29 +188,27 @@ extern "C" int qie_vae_rms_norm_bf16(const void* x, const void* gamma, void* y, 
                                      int silu, qie_stream_t stream) {
   QIE_CHECK_ARG(x && gamma && y && pixels > 0 && C > 0 && C % 8 == 0 && C <= 512);
   QIE_CHECK_ARG(((uintptr_t)x % 16) == 0 && ((uintptr_t)y % 16) == 0 && ((uintptr_t)gamma % 16) == 0);
-  const unsigned grid = (unsigned)((pixels + 3) / 4);
   const float scale = sqrtf((float)C);
-  if (silu)
-    rms_norm_kernel<true><<<grid, 256, 0, (hipStream_t)stream>>>((const bf16_t*)x, (const bf16_t*)gamma,
-                                                                 (bf16_t*)y, pixels, C, scale);
-  else
-    rms_norm_kernel<false><<<grid, 256, 0, (hipStream_t)stream>>>((const bf16_t*)x, (const bf16_t*)gamma,
-                                                                  (bf16_t*)y, pixels, C, scale);
+  const hipStream_t st = (hipStream_t)stream;
+  const bf16_t *xb = (const bf16_t*)x, *gb = (const bf16_t*)gamma;
+  bf16_t* yb = (bf16_t*)y;
+  auto launch = [&](auto g_t) {
+    constexpr int G = decltype(g_t)::value;
+    const unsigned grid = (unsigned)((pixels * G + 255) / 256);
+    if (silu) rms_norm_kernel<true, G><<<grid, 256, 0, st>>>(xb, gb, yb, pixels, C, scale);
+    else rms_norm_kernel<false, G><<<grid, 256, 0, st>>>(xb, gb, yb, pixels, C, scale);
+  };
+  if (C <= 128) launch(std::integral_constant<int, 16>{});
+  else if (C <= 256) launch(std::integral_constant<int, 32>{});
+  else launch(std::integral_constant<int, 64>{});
   return qie_last_error();
 }
 
-extern "C" int qie_softmax_rows_f32_bf16(const float* s, void* p, int rows, int N, float scale,
-                                         qie_stream_t stream) {
-  QIE_CHECK_ARG(s && p && rows > 0 && N > 0 && N % 1024 == 0 && N <= 16384);
-  const hipStream_t st = (hipStream_t)stream;
-  switch (N / 256) {
-    case 4: softmax_rows_kernel<4><<<rows, 256, 0, st>>>(s, (bf16_t*)p, N, scale); break;
-    case 8: softmax_rows_kernel<8><<<rows, 256, 0, st>>>(s, (bf16_t*)p, N, scale); break;
-    case 16: softmax_rows_kernel<16><<<rows, 256, 0, st>>>(s, (bf16_t*)p, N, scale); break;
-    case 32: softmax_rows_kernel<32><<<rows, 256, 0, st>>>(s, (bf16_t*)p, N, scale); break;
-    case 64: softmax_rows_kernel<64><<<rows, 256, 0, st>>>(s, (bf16_t*)p, N, scale); break;
-    default: return QIE_ERR_UNSUPPORTED;
-  }
+extern "C" int qie_softmax_rows_f32_bf16(const float* s, int64_t lds, void* p, int64_t ldp, int rows, int N,
+                                         float scale, qie_stream_t stream) {
+  QIE_CHECK_ARG(s && p && rows > 0 && N > 0 && N % 4 == 0 && lds >= N && lds % 4 == 0);
+  QIE_CHECK_ARG(ldp >= N && ldp % 4 == 0 && ((uintptr_t)s % 16) == 0 && ((uintptr_t)p % 8) == 0);
+  softmax_rows_kernel<<<rows, 256, 0, (hipStream_t)stream>>>(s, lds, (bf16_t*)p, ldp, N, scale);
   return qie_last_error();
 }
 

@@ -473,13 +473,15 @@ def matmul_f32out(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] 
 
 
 def softmax_rows(s: torch.Tensor, scale: float, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """bf16 softmax(scale * s) per row of fp32 s [R, N]; ``out`` [R, >=N] (a row-major view whose
+    columns past N -- the K padding of a following GEMM -- are zero-filled)."""
     _dev(s, out)
-    _chk(s.dtype == torch.float32 and s.dim() == 2 and s.is_contiguous(), "fp32 [rows, N]")
+    _chk(s.dtype == torch.float32 and _is2d_rowmajor(s), "fp32 [rows, N]")
     R, N = s.shape
     if out is None:
         out = torch.empty(R, N, dtype=BF16, device=s.device)
-    _chk(out.shape == (R, N) and out.is_contiguous() and out.dtype == BF16, "out")
-    _lib.call("qie_softmax_rows_f32_bf16", _p(s), _p(out), R, N, scale, _stream())
+    _chk(_is2d_rowmajor(out) and out.shape[0] == R and out.shape[1] >= N and out.dtype == BF16, "out")
+    _lib.call("qie_softmax_rows_f32_bf16", _p(s), s.stride(0), _p(out), out.shape[1], R, N, scale, _stream())
     return out
 
 

@@ -13,11 +13,12 @@ FlowMatch schedule, and the denoise loop with **batched CFG** (a3, the absent
 ``batched_cfg_pipeline.py`` of README.md:126: cond and uncond stacked on the
 batch axis in ONE forward, unequal text lengths key-masked so the result equals
 the reference's two sequential forwards), the true-CFG norm rescale (a2) and
-the Euler step.  The text encoder (Qwen2.5-VL) and VAE are §8(f) "next" rows;
-until they land, callers pass ``prompt_embeds`` / ``image_latents`` directly
-or plug encoders in through ``prompt_encoder`` / ``image_encoder`` /
-``latent_decoder`` hooks.  ``output_type="latent"`` returns packed latents,
-as diffusers does.
+the Euler step, then the VAE decode (§8 f1, ``vae.QwenImageVAEDecoder``: unpack,
+de-normalise, decoder, uint8 RGB, all on the HIP path).  The text encoder
+(Qwen2.5-VL, §8 f2) and the VAE *encoder* are still "next": callers pass
+``prompt_embeds`` / ``image_latents`` directly or plug encoders in through the
+``prompt_encoder`` / ``image_encoder`` hooks (``latent_decoder`` overrides the
+HIP decoder).  ``output_type="latent"`` returns packed latents, as diffusers does.
 """
 from __future__ import annotations
 
@@ -30,6 +31,7 @@ import torch
 from . import ops
 from .scheduler import FlowMatchEulerDiscreteScheduler, calculate_shift, model_timesteps
 from .transformer import QwenImageTransformer2DModel
+from .vae import QwenImageVAEDecoder
 from . import weights as W
 
 BF16 = torch.bfloat16
@@ -48,6 +50,20 @@ def calculate_dimensions(target_area: int, ratio: float) -> Tuple[int, int]:
 @dataclass
 class QwenImagePipelineOutput:
     images: Any
+
+
+def to_output(rgb: torch.Tensor, output_type: str):
+    """uint8 RGB [B, H, W, 3] (device) -> the image processor's output types: "pil" (list of
+    PIL.Image), "np" (float [B, H, W, 3] in [0, 1]), "pt" (float [B, 3, H, W] in [0, 1]), "uint8"."""
+    if output_type == "uint8":
+        return rgb
+    if output_type == "pt":
+        return rgb.permute(0, 3, 1, 2).float() / 255.0
+    arr = rgb.cpu().numpy()
+    if output_type == "np":
+        return arr.astype("float32") / 255.0
+    from PIL import Image
+    return [Image.fromarray(a) for a in arr]
 
 
 class QwenImageEditPlusPipeline:
@@ -89,7 +105,12 @@ class QwenImageEditPlusPipeline:
                 "pass a local directory or random_init_seed=")
         if int8:
             model.quantize_int8()
-        return cls(model)
+        pipe = cls(model)
+        if path is not None and W.find_vae_files(path):
+            pipe.vae = W.load_vae_decoder(path, device=device)
+        elif random_init_seed is not None or path is None:
+            pipe.vae = QwenImageVAEDecoder(device=device).random_init_(seed=(random_init_seed or 0) + 1)
+        return pipe
 
     def to(self, device=None, *a, **k):
         return self
@@ -224,12 +245,13 @@ class QwenImageEditPlusPipeline:
         ops.copy_batched(inp[:B, :S_noise], final)
         if output_type == "latent":
             images = final
-        else:
-            if self.latent_decoder is None:
-                raise NotImplementedError(
-                    "VAE decode (SURVEY.md §8 f1) is not on the HIP hot path yet: use output_type='latent' "
-                    "or set pipe.latent_decoder")
+        elif self.latent_decoder is not None:
             images = self.latent_decoder(final, 2 * lh, 2 * lw)
+        elif self.vae is not None:  # HIP VAE decoder (vae.py): uint8 RGB [B, H, W, 3] on the device
+            images = to_output(self.vae.decode(final, 2 * lh, 2 * lw), output_type)
+        else:
+            raise NotImplementedError("no VAE decoder: load a snapshot with vae/, set pipe.vae / "
+                                      "pipe.latent_decoder, or use output_type='latent'")
         if not return_dict:
             return (images,)
         return QwenImagePipelineOutput(images=images)

@@ -227,13 +227,19 @@ class QwenRealtimePipeline:
         self.image_encoder = image_encoder
         self.prompt_encoder = prompt_encoder
         self.latent_decoder = latent_decoder
+        self.vae = None  # vae.QwenImageVAEDecoder: finished frames come out as uint8 RGB [H, W, 3]
         self.generator: Optional[torch.Generator] = None
 
     def load_model(self, transformer: Optional[QwenImageTransformer2DModel] = None, seed: int = 0,
-                   **config_overrides):
+                   vae=None, **config_overrides):
+        """``vae``: a QwenImageVAEDecoder, or "random" for a seeded random one (benchmarks)."""
         if transformer is None:
             transformer = QwenImageTransformer2DModel(**config_overrides).random_init_(seed)
         self.transformer = transformer
+        if isinstance(vae, str) and vae == "random":
+            from .vae import QwenImageVAEDecoder
+            vae = QwenImageVAEDecoder(device=transformer.device).random_init_(seed + 1)
+        self.vae = vae
         self.generator = torch.Generator(device=transformer.device).manual_seed(42)
 
     def precompute_conditions(self, prompt: str, reference_image=None, prompt_embeds=None,
@@ -283,6 +289,9 @@ class QwenRealtimePipeline:
             self.prev_latent = out
             if self.latent_decoder is not None:
                 out = self.latent_decoder(out, *self.config.output_size)
+            elif self.vae is not None:  # qwen_realtime.py:188-199 decode_latent, on the HIP path
+                oh, ow = self.config.output_size
+                out = self.vae.decode(out, oh // 8, ow // 8)[0]
         self.inference_times.append(time.time() - t0)
         return out
 

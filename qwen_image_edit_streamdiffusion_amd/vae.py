@@ -203,8 +203,10 @@ class QwenImageVAEDecoder:
             self._ws[key] = {
                 "a": torch.empty(n, **e), "b": torch.empty(n, **e), "t": torch.empty(n, **e), "y": torch.empty(n, **e),
                 "z": torch.empty(P0, 16, **e), "qkv": torch.empty(P0, 3 * C0, **e),
-                "s": torch.empty(P0, P0, dtype=torch.float32, device=dev), "p": torch.empty(P0, P0, **e),
-                "vt": torch.empty(C0, P0, **e), "att": torch.empty(P0, C0, **e),
+                # mid-block attention: K of P.V padded to 64 (zero P columns, zero V^T columns)
+                "s": torch.empty(P0, P0, dtype=torch.float32, device=dev),
+                "p": torch.empty(P0, -(-P0 // 64) * 64, **e),
+                "vt": torch.zeros(C0, -(-P0 // 64) * 64, **e), "att": torch.empty(P0, C0, **e),
                 "zero_b": torch.zeros(C0, **e),
                 "out": torch.empty(P, 4, **e),
             }
@@ -238,19 +240,17 @@ class QwenImageVAEDecoder:
         """QwenImageAttentionBlock: x += proj(SDPA(to_qkv(norm(x)))), one head over H*W tokens."""
         P = H * W
         wt = self.w
-        if P % 1024 or P > 16384:
-            raise NotImplementedError("mid-block attention: H*W must be a multiple of 1024, <= 16384")
         t = self._view(ws["t"], P, C)
         ops.vae_rms_norm(x, wt[f"{prefix}.norm.gamma"], False, out=t)
         qkv = ws["qkv"][:P]
         ops.conv2d(t, H, W, wt[f"{prefix}.to_qkv.weight"], wt[f"{prefix}.to_qkv.bias"], ksize=1, out=qkv)
         q, k, v = qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:]
-        s = ws["s"][:P, :P]
+        s = ws["s"]
         ops.matmul_f32out(q, k, out=s)
-        p = ws["p"][:P, :P]
+        p = ws["p"]  # [P, roundup(P, 64)], zero past column P
         ops.softmax_rows(s, 1.0 / math.sqrt(C), out=p)
-        vt = ws["vt"][:, :P]
-        ops.transpose(v, out=vt)
+        vt = ws["vt"]  # [C, roundup(P, 64)], zero past column P
+        ops.transpose(v, out=vt[:, :P])
         att = ws["att"][:P]
         ops.linear(p, vt, ws["zero_b"][:C], out=att)
         ops.conv2d(att, H, W, wt[f"{prefix}.proj.weight"], wt[f"{prefix}.proj.bias"], ksize=1, out=x, residual=True)

@@ -182,3 +182,39 @@ def load_int8(path: str, device="cuda"):
             for k in fh.keys():
                 sd[k] = fh.get_tensor(k).to(device)
     return model.load_int8_state_dict(sd)
+
+
+# ---------------------------------------------------------------------------- VAE (§8 f1)
+def find_vae_files(path: str):
+    """VAE safetensors of a diffusers snapshot (``vae/*.safetensors``)."""
+    return sorted(glob.glob(os.path.join(path, "vae", "*.safetensors"))) if os.path.isdir(path) else []
+
+
+def load_vae_decoder(path: str, device="cuda"):
+    """QwenImageVAEDecoder from a diffusers snapshot: ``vae/config.json`` (dims, latents_mean /
+    latents_std) and the decode half of the AutoencoderKLQwenImage state_dict (``decoder.*``,
+    ``post_quant_conv.*``; the encoder keys are skipped without being read)."""
+    import json
+    from .vae import QwenImageVAEDecoder, VAEConfig
+    cfg = VAEConfig()
+    cj = os.path.join(path, "vae", "config.json")
+    if os.path.isfile(cj):
+        with open(cj) as fh:
+            c = json.load(fh)
+        for k in ("base_dim", "z_dim", "num_res_blocks"):
+            if k in c:
+                setattr(cfg, k, int(c[k]))
+        for k in ("dim_mult", "temperal_downsample", "latents_mean", "latents_std"):
+            if k in c:
+                setattr(cfg, k, tuple(c[k]))
+    files = find_vae_files(path)
+    if not files:
+        raise FileNotFoundError(f"no vae/*.safetensors under {path}")
+    from safetensors import safe_open
+    sd = {}
+    for f in files:
+        with safe_open(f, framework="pt", device="cpu") as fh:
+            for k in fh.keys():
+                if k.startswith("decoder.") or k.startswith("post_quant_conv."):
+                    sd[k] = fh.get_tensor(k)
+    return QwenImageVAEDecoder(cfg, device).load_state_dict(sd)

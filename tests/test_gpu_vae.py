@@ -51,6 +51,8 @@ def _nhwc(x):  # [C, H, W] -> [H*W, C]
     (8, 16, 384, 192, 3, True),     # Resample: upsample folded into the gather
     (16, 16, 192, 384, 1, False),   # conv_shortcut 1x1
     (24, 20, 96, 4, 3, False),      # conv_out: 3 (+1 pad) channels, ragged tiles
+    (128, 256, 64, 512, 3, False),  # 256-pixel tiles (8 waves): >= 512 workgroups
+    (64, 128, 96, 384, 3, True),    # 256-pixel tiles through the upsampling gather
 ])
 def test_conv2d(dev, H, W, C, N, k, up):
     from qwen_image_edit_streamdiffusion_amd.vae import conv_weight
@@ -112,6 +114,12 @@ def test_softmax_transpose_matmul(dev):
     close(p, torch.softmax(sref / math.sqrt(C), -1))
     vt = ops.transpose(v)
     assert torch.equal(vt.cpu(), v.cpu().T)
+    # ragged row length into a K-padded output: zeros past column N
+    s2 = s[:100, :1000].contiguous()
+    out = torch.full((100, 1024), float("nan"), device=dev).to(BF16)
+    ops.softmax_rows(s2, 0.05, out=out)
+    close(out[:, :1000], torch.softmax(sref[:100, :1000] * 0.05, -1))
+    assert (out[:, 1000:] == 0).all()
 
 
 def test_vae_latents_in(dev):
@@ -156,6 +164,19 @@ def test_vae_decode_vs_oracle(dev):
     assert (u8.cpu().float() - ru8.float()).abs().mean().item() <= 1.5
 
 
+def test_vae_decode_ragged_latent(dev):
+    """18 x 22 latents: mid-block attention over 396 tokens (P.V K padded to 448), ragged tiles."""
+    from qwen_image_edit_streamdiffusion_amd.vae import QwenImageVAEDecoder, VAEConfig
+    dec = QwenImageVAEDecoder(VAEConfig(base_dim=16), dev).random_init_(6)
+    h, w = 18, 22
+    packed = rnd((1, h * w // 4, 64), dev, 1.0, 15)
+    img = dec.decode(packed, h, w, output="pt")[0]
+    p = V.random_params(V.VAEConfig(base_dim=16), 6)
+    ref = V.decode(p, packed.cpu(), h, w, V.VAEConfig(base_dim=16), emulate_bf16=True)[0]
+    err = ((img.float().cpu() - ref).norm() / ref.norm()).item()
+    assert err <= 3e-2, err
+
+
 def test_vae_decode_deterministic_and_batch_independent(dev):
     dec, packed, _, h, w = _small_decode(dev, 13)
     two = torch.cat([packed, rnd(packed.shape, dev, 1.0, 14)]).contiguous()
@@ -163,3 +184,31 @@ def test_vae_decode_deterministic_and_batch_independent(dev):
     b = dec.decode(packed, h, w)
     assert torch.equal(a[:1], b)
     assert torch.equal(dec.decode(packed, h, w), b)
+
+
+def test_pipeline_decodes_with_hip_vae(dev):
+    """QwenImageEditPlusPipeline with pipe.vae set: output_type pil / np / pt / uint8 all come from
+    the HIP decode of the same final latents (output_type="latent")."""
+    from oracle import dit_ref as R
+    from qwen_image_edit_streamdiffusion_amd import QwenImageEditPlusPipeline, QwenImageTransformer2DModel
+    from qwen_image_edit_streamdiffusion_amd.vae import QwenImageVAEDecoder, VAEConfig
+    cfg = R.tiny_config()
+    m = QwenImageTransformer2DModel(num_layers=cfg.num_layers, num_attention_heads=cfg.num_attention_heads,
+                                    joint_attention_dim=cfg.joint_attention_dim, device=dev)
+    m.load_diffusers_state_dict(R.random_params(cfg, seed=0))
+    pipe = QwenImageEditPlusPipeline(m)
+    pipe.vae = QwenImageVAEDecoder(VAEConfig(base_dim=16), dev).random_init_(7)
+    g = torch.Generator().manual_seed(8)
+    pe = torch.randn(1, 20, cfg.joint_attention_dim, generator=g).to(BF16).to(dev)
+    cond = torch.randn(1, 64, 64, generator=g).to(BF16).to(dev)
+    kw = dict(prompt_embeds=pe, image_latents=cond, num_inference_steps=2, height=128, width=128)
+    lat = pipe(generator=torch.Generator().manual_seed(42), output_type="latent", **kw).images
+    u8 = pipe(generator=torch.Generator().manual_seed(42), output_type="uint8", **kw).images
+    assert u8.shape == (1, 128, 128, 3) and u8.dtype == torch.uint8
+    assert torch.equal(u8, pipe.vae.decode(lat, 16, 16))
+    pil = pipe(generator=torch.Generator().manual_seed(42), **kw).images
+    assert len(pil) == 1 and pil[0].size == (128, 128)
+    import numpy as np
+    assert np.array_equal(np.asarray(pil[0]), u8[0].cpu().numpy())
+    pt = pipe(generator=torch.Generator().manual_seed(42), output_type="pt", **kw).images
+    assert pt.shape == (1, 3, 128, 128) and torch.allclose(pt * 255, u8.permute(0, 3, 1, 2).float())
