@@ -8,15 +8,20 @@ of depth 2 (= the 2 Lightning steps), cond-only (the server's default
 use_cfg=False path, server.py:49,147-153), prompt-embed cache, 1024^2 output
 (4096 noise tokens) + 1024^2 condition image (4096 tokens) + 216 text tokens.
 One "step" = one pushed frame = one batched B=2 DiT forward + per-row Euler
-step; in steady state every step completes one image, so images/sec =
-completed frames / time.  Synthetic inputs (randn with fixed seeds) are
-resident in HBM before the timed region.  The VAE and the text encoder are
-not part of this path.
+step, then the VAE decode of the frame that completed (HIP decoder, SURVEY.md
+§8 f1: unpack + de-normalise + post_quant_conv + QwenImageDecoder3d + uint8 RGB
+1024x1024x3 on the device; --no-decode leaves the latents); in steady state
+every step completes one image, so images/sec = completed frames / time.
+Synthetic inputs (randn with fixed seeds) are resident in HBM before the timed
+region.  The VAE encoder of the condition frame and the text encoder are not
+part of this path yet (the condition arrives as latents, the prompt embedding
+comes from the prompt cache).
 
 Multi-GPU (torch.distributed.run, one process per GPU, RCCL): each rank runs
 its own stream engine on its own frames (frame shard, weak scaling); rank 0
-broadcasts the prompt embeddings once and gathers every finished latent
-(512 KiB / frame) inside the timed loop.  value = frames of all ranks / max
+broadcasts the prompt embeddings once and gathers every finished image
+(uint8 RGB, 3 MiB / frame; the 512 KiB latent with --no-decode) inside the
+timed loop.  value = frames of all ranks / max
 rank time.
 
 Also emitted: roofline of the dominant kernel (HIP events around each launch
@@ -51,7 +56,7 @@ def log(*a):
         print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(budget_note: str = ""):
+def cpu_baseline(decode: bool = True):
     """Oracle (torch fp32 on the host cores) on a bounded sample of the SAME
     workload: one B=2 stream-batch forward with 1 of the 60 blocks (prologue +
     block + head) at full size, scaled x60 -> sec/image (1 forward/image)."""
@@ -69,10 +74,20 @@ def cpu_baseline(budget_note: str = ""):
     R.transformer_forward(params, cfg, hs, enc, t, shapes, [S_TXT, S_TXT], emulate_bf16=False)
     dt = time.time() - t0
     sec_per_image = dt * 60
+    sample = (f"oracle fp32 torch-CPU: one B=2 stream-batch forward with 1 of 60 DiT blocks at full 1024^2 size "
+              f"({dt:.1f} s), scaled x60")
+    if decode:  # VAE decode of the real architecture at 32x32 latents (256^2), scaled by FLOPs to 128x128
+        from oracle import vae_ref as V
+        vc = V.VAEConfig()
+        vp = V.random_params(vc, 1)
+        packed = torch.randn(1, 256, 64, generator=g).to(BF16)
+        t0 = time.time()
+        V.decode(vp, packed, 32, 32, vc, emulate_bf16=False)
+        dv = (time.time() - t0) * V.decode_flops(vc, 128, 128) / V.decode_flops(vc, 32, 32)
+        sec_per_image += dv
+        sample += f" + VAE decode (256^2 sample, FLOP-scaled to 1024^2: {dv:.1f} s)"
     return {"value": 1.0 / sec_per_image, "unit": "images/sec", "cores": n, "kind": "port",
-            "sample": "oracle fp32 torch-CPU: one B=2 stream-batch forward with 1 of 60 DiT blocks at "
-                      f"full 1024^2 size ({dt:.1f} s), scaled x60 = {sec_per_image:.0f} s/image",
-            "sec_per_image": sec_per_image}
+            "sample": sample + f" = {sec_per_image:.0f} s/image", "sec_per_image": sec_per_image}
 
 
 @contextlib.contextmanager
@@ -98,6 +113,8 @@ def main():
     ap.add_argument("--workload", default="stream2", choices=["stream2", "stream2-int8", "stream2-cfg", "cfg4"])
     ap.add_argument("--layers", type=int, default=60, help="debug only; the headline needs 60")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-decode", action="store_true",
+                    help="stop at the finished latents (no VAE decode inside the timed step)")
     ap.add_argument("--no-probe", action="store_true")
     ap.add_argument("--no-qk-fusion", action="store_true",
                     help="A/B: image QKV GEMM and QK RMSNorm+RoPE as two launches")
@@ -128,6 +145,7 @@ def main():
 
     from qwen_image_edit_streamdiffusion_amd import (QwenImageTransformer2DModel, StreamBatchDenoiser,
                                                      QwenImageEditPlusPipeline)
+    from qwen_image_edit_streamdiffusion_amd.vae import QwenImageVAEDecoder
     t_build = time.time()
     model = QwenImageTransformer2DModel(num_layers=args.layers, device=dev).random_init_(seed=0)
     if args.workload == "stream2-int8":
@@ -136,6 +154,8 @@ def main():
     model.fuse_qk_norm_rope = not args.no_qk_fusion
     model.log2q_attention = not args.no_log2q
     model.text_splits = args.text_splits or None
+    decode = not args.no_decode
+    vae = QwenImageVAEDecoder(device=dev).random_init_(seed=1) if decode else None
     torch.cuda.synchronize()
     log(f"[bench] model built in {time.time() - t_build:.1f}s, "
         f"{torch.cuda.memory_allocated() / 1e9:.1f} GB")
@@ -171,23 +191,28 @@ def main():
         rows = 2
         fwd_per_step = 4
 
+        pipe.vae = vae
+
         def step(i):
             return pipe(prompt_embeds=pe, negative_prompt_embeds=ne, image_latents=conds[i % nf],
                         latents=noises[i % nf], true_cfg_scale=4.0, num_inference_steps=4,
-                        output_type="latent").images
+                        output_type="uint8" if decode else "latent").images
 
     gather_buf = None
     if dist_on and rank == 0:
-        gather_buf = [torch.empty(1, S_NOISE, 64, dtype=BF16, device=dev) for _ in range(world)]
+        gather_buf = [torch.empty(1, 1024, 1024, 3, dtype=torch.uint8, device=dev) if decode else
+                      torch.empty(1, S_NOISE, 64, dtype=BF16, device=dev) for _ in range(world)]
 
     def deliver(res):
+        out = res[1] if isinstance(res, tuple) else res
+        if decode and out.dtype != torch.uint8:  # stream engine: decode the frame that completed
+            out = vae.decode(out, 128, 128)
         if dist_on:
-            lat = res[1] if isinstance(res, tuple) else res
-            dist.gather(lat, gather_buf if rank == 0 else None, dst=0)
+            dist.gather(out, gather_buf if rank == 0 else None, dst=0)
 
     for i in range(args.warmup):
         r = step(i)
-        if r is not None and i >= 1:
+        if r is not None:
             deliver(r)
     if args.workload.startswith("stream2") and args.warmup < 2:
         step(args.warmup)  # fill the 2-deep pipeline
@@ -222,7 +247,7 @@ def main():
     sec_per_image = el * world / max(images, 1)
     S = S_NOISE + S_COND + S_TXT
     flops_fwd = model.flops_per_forward(S_NOISE + S_COND, S_TXT, B=rows)
-    flops_img = flops_fwd * fwd_per_step
+    flops_img = flops_fwd * fwd_per_step + (vae.flops(128, 128) if decode else 0.0)
     peak = PEAK_I8 if args.workload.endswith("int8") else PEAK_BF16
 
     kernels = {}
@@ -259,7 +284,7 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
-            cpu = cpu_baseline()
+            cpu = cpu_baseline(decode)
         except Exception as e:  # reported, never fatal to the GPU number
             cpu = {"error": repr(e)}
 
@@ -270,14 +295,17 @@ def main():
                     "stream2-cfg": "lightning-2step stream-batch depth=2 + true-CFG 4.0 (B=4), 1024x1024",
                     "cfg4": "4-step true-CFG 4.0 batched cond/uncond, 1024x1024 (configs[1])"}[args.workload]
         line = {
-            "metric": "images/sec, 1024x1024 2-step Lightning edit (DiT denoise)",
+            "metric": "images/sec, 1024x1024 2-step Lightning edit (DiT denoise" +
+                      (" + VAE decode)" if decode else ")"),
             "value": value, "unit": "images/sec", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None,
             "dtype": "int8" if args.workload.endswith("int8") else "bf16",
             "data": "synthetic (randn latents/cond/prompt embeds; random-init weights of the real "
                     "60-block architecture)",
-            "config": {"workload": workload, "model": "Qwen-Image-Edit-2509 DiT (60 blocks, D=3072)",
+            "config": {"workload": workload,
+                       "model": "Qwen-Image-Edit-2509 DiT (60 blocks, D=3072)" +
+                                (" + AutoencoderKLQwenImage decoder" if decode else ""),
                        "global_batch": rows * world, "seq_len": S, "layers": args.layers,
                        "parallelism": f"frame-shard x{world}" if world > 1 else "single"},
             "sec_per_image": sec_per_image,
