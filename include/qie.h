@@ -276,12 +276,14 @@ int qie_linear_splitk_i8(const void* xq, int64_t ldx, const float* sx, const voi
  * with the last temporal slice of its kernel; Resample "upsample3d" skips its time_conv on the
  * first frame. Activations are NHWC bf16 [pixels][C]. */
 
-/* 3x3 (pad 1) or 1x1 convolution as an implicit GEMM: y[p][n] = bf16(sum_{tap,c} x[shift(p, tap)][c]
- * * w[n][tap*C + c] + bias[n]) with the input gathered per tap (no im2col buffer); up = 1 folds a
- * nearest-2x upsample into the gather (output H_in*2 x W_in*2). w: [N][ldw] bf16, K order
- * [ky][kx][C], zero-padded to ldw >= roundup(ksize^2 * C, 64). resid != NULL (must equal y):
- * y = bf16(y + bf16(acc + bias)) (ResidualBlock x + h). C % 8 == 0, N % 4 == 0. */
-int qie_conv2d_bf16(const void* x, int H_in, int W_in, int C, int up, int ksize, const void* w, int64_t ldw,
+/* 3x3 or 1x1 convolution as an implicit GEMM: y[p][n] = bf16(sum_{tap,c} x[src(p, tap)][c]
+ * * w[n][tap*C + c] + bias[n]) with the input gathered per tap (no im2col buffer). mode 0: same
+ * size, pad ksize/2; 1: a nearest-2x upsample folded into the gather (decoder Resample, output
+ * 2H x 2W); 2: stride 2 after ZeroPad2d((0,1,0,1)) (encoder Resample, output H/2 x W/2, 3x3).
+ * w: [N][ldw] bf16, K order [ky][kx][C], zero-padded to ldw >= roundup(ksize^2 * C, 64).
+ * resid != NULL (must equal y): y = bf16(y + bf16(acc + bias)) (ResidualBlock x + h).
+ * C % 8 == 0, N % 4 == 0. */
+int qie_conv2d_bf16(const void* x, int H_in, int W_in, int C, int mode, int ksize, const void* w, int64_t ldw,
                     const void* bias, const void* resid, void* y, int N, qie_stream_t stream);
 
 /* y[M][N] = x[M][K] . w[N][K]^T as raw fp32 (row strides ldx, ldw elements): attention scores of
@@ -307,6 +309,16 @@ int qie_softmax_rows_f32_bf16(const float* s, int64_t lds, void* p, int64_t ldp,
 
 /* y[c][r] = x[r][c] for an R x C bf16 block (row strides ldx, ldy elements). */
 int qie_transpose_bf16(const void* x, int64_t ldx, void* y, int64_t ldy, int R, int C, qie_stream_t stream);
+
+/* Encoder input: uint8 RGB [pixels][3] -> bf16(2 v/255 - 1) (VaeImageProcessor.preprocess, then
+ * .to(bf16)) as NHWC [pixels][8], channels 3..7 zero (the conv gather reads 8-channel chunks). */
+int qie_vae_rgb_in(const void* rgb, void* y, int64_t pixels, qie_stream_t stream);
+
+/* Encoder output: quant_conv result NHWC [batch][h][w][ldx] bf16 -> its mode (channels 0..15, the
+ * DiagonalGaussian mean; retrieve_latents(sample_mode="argmax")) -> bf16(bf16(mu - mean) / std)
+ * -> packed [batch][(h/2)(w/2)][64] (_encode_vae_image + _pack_latents). */
+int qie_vae_latents_out_bf16(const void* x, int64_t ldx, int batch, int h, int w, const void* mean,
+                             const void* stdv, void* packed, qie_stream_t stream);
 
 /* Decoder output [pixels][ldx] bf16 (channels 0..2) -> clamp(-1, 1) -> (x/2 + 0.5).clamp(0, 1)
  * -> round(255 v) as uint8 RGB [pixels][3] (VaeImageProcessor.postprocess, output_type="pil"). */

@@ -264,3 +264,111 @@ def decode_flops(cfg: VAEConfig, h: int, w: int) -> float:
             f += conv(b, b // 2, 3, H, W)
     f += conv(d[-1], 3, 3, H, W)
     return f
+
+
+# ---------------------------------------------------------------------------- encoder
+def encoder_param_shapes(cfg: VAEConfig) -> Dict[str, Tuple[int, ...]]:
+    """diffusers names/shapes of the encode path: QwenImageEncoder3d (``encoder.*``; down_blocks is
+    one flat ModuleList of resnets and Resample downsamplers) and ``quant_conv`` [U]."""
+    dims = [cfg.base_dim * u for u in [1] + list(cfg.dim_mult)]
+    z2 = 2 * cfg.z_dim
+    s: Dict[str, Tuple[int, ...]] = {"encoder.conv_in.weight": (dims[0], 3, 3, 3, 3), "encoder.conv_in.bias": (dims[0],)}
+
+    def res(prefix, a, b):
+        s[f"{prefix}.norm1.gamma"] = (a, 1, 1, 1)
+        s[f"{prefix}.conv1.weight"] = (b, a, 3, 3, 3)
+        s[f"{prefix}.conv1.bias"] = (b,)
+        s[f"{prefix}.norm2.gamma"] = (b, 1, 1, 1)
+        s[f"{prefix}.conv2.weight"] = (b, b, 3, 3, 3)
+        s[f"{prefix}.conv2.bias"] = (b,)
+        if a != b:
+            s[f"{prefix}.conv_shortcut.weight"] = (b, a, 1, 1, 1)
+            s[f"{prefix}.conv_shortcut.bias"] = (b,)
+
+    idx = 0
+    for i, (a, b) in enumerate(zip(dims[:-1], dims[1:])):
+        for _ in range(cfg.num_res_blocks):
+            res(f"encoder.down_blocks.{idx}", a, b)
+            idx += 1
+            a = b
+        if i != len(cfg.dim_mult) - 1:
+            s[f"encoder.down_blocks.{idx}.resample.1.weight"] = (b, b, 3, 3)
+            s[f"encoder.down_blocks.{idx}.resample.1.bias"] = (b,)
+            if cfg.temperal_downsample[i]:
+                s[f"encoder.down_blocks.{idx}.time_conv.weight"] = (b, b, 3, 1, 1)
+                s[f"encoder.down_blocks.{idx}.time_conv.bias"] = (b,)
+            idx += 1
+    top = dims[-1]
+    res("encoder.mid_block.resnets.0", top, top)
+    res("encoder.mid_block.resnets.1", top, top)
+    a = "encoder.mid_block.attentions.0"
+    s[f"{a}.norm.gamma"] = (top, 1, 1)
+    s[f"{a}.to_qkv.weight"] = (3 * top, top, 1, 1)
+    s[f"{a}.to_qkv.bias"] = (3 * top,)
+    s[f"{a}.proj.weight"] = (top, top, 1, 1)
+    s[f"{a}.proj.bias"] = (top,)
+    s["encoder.norm_out.gamma"] = (top, 1, 1, 1)
+    s["encoder.conv_out.weight"] = (z2, top, 3, 3, 3)
+    s["encoder.conv_out.bias"] = (z2,)
+    s["quant_conv.weight"] = (z2, z2, 1, 1, 1)
+    s["quant_conv.bias"] = (z2,)
+    return s
+
+
+def random_encoder_params(cfg: VAEConfig, seed: int = 0) -> Dict[str, torch.Tensor]:
+    g = torch.Generator().manual_seed(seed)
+    out = {}
+    for name, shp in encoder_param_shapes(cfg).items():
+        if name.endswith("gamma"):
+            t = 1.0 + 0.05 * torch.randn(shp, generator=g)
+        elif name.endswith("bias"):
+            t = 0.02 * torch.randn(shp, generator=g)
+        else:
+            t = torch.randn(shp, generator=g) / math.sqrt(math.prod(shp[1:]))
+        out[name] = t.to(BF16)
+    return out
+
+
+def resample_down(p, prefix: str, x: torch.Tensor, r: _R) -> torch.Tensor:
+    """QwenImageResample downsample2d / downsample3d on the first frame (time_conv skipped: its
+    feat_cache entry starts empty) [U]: ZeroPad2d((0, 1, 0, 1)) + Conv2d(dim, dim, 3, stride=2)."""
+    B, C, T, H, W = x.shape
+    xi = x.permute(0, 2, 1, 3, 4).reshape(B * T, C, H, W)
+    xi = F.pad(xi, (0, 1, 0, 1))
+    y = r(F.conv2d(xi, p[f"{prefix}.resample.1.weight"].float(), p[f"{prefix}.resample.1.bias"].float(), stride=2))
+    return y.view(B, T, C, y.shape[2], y.shape[3]).permute(0, 2, 1, 3, 4)
+
+
+def pack_latents(z: torch.Tensor) -> torch.Tensor:
+    """_pack_latents: [B, 16, 1, h, w] -> [B, (h/2)(w/2), 64] [U]."""
+    B, C, _, h, w = z.shape
+    return z.view(B, C, h // 2, 2, w // 2, 2).permute(0, 2, 4, 1, 3, 5).reshape(B, (h // 2) * (w // 2), C * 4)
+
+
+def encode(p: Dict[str, torch.Tensor], rgb: torch.Tensor, cfg: VAEConfig = VAEConfig(), emulate_bf16: bool = True,
+           mean=LATENTS_MEAN, std=LATENTS_STD) -> torch.Tensor:
+    """uint8 RGB [B, H, W, 3] -> packed normalised condition latents [B, (H/16)(W/16), 64]:
+    preprocess (2 v/255 - 1, bf16), vae.encode (encoder + quant_conv), mode, (mu - mean) / std."""
+    r = _R(emulate_bf16)
+    x = r(2.0 * (rgb.float() / 255.0) - 1.0).permute(0, 3, 1, 2)[:, :, None]
+    x = causal_conv3d(x, p["encoder.conv_in.weight"], p["encoder.conv_in.bias"], 1, r)
+    dims = [cfg.base_dim * u for u in [1] + list(cfg.dim_mult)]
+    idx = 0
+    for i in range(len(dims) - 1):
+        for _ in range(cfg.num_res_blocks):
+            x = residual_block(p, f"encoder.down_blocks.{idx}", x, r)
+            idx += 1
+        if i != len(cfg.dim_mult) - 1:
+            x = resample_down(p, f"encoder.down_blocks.{idx}", x, r)
+            idx += 1
+    x = residual_block(p, "encoder.mid_block.resnets.0", x, r)
+    x = attention_block(p, "encoder.mid_block.attentions.0", x, r)
+    x = residual_block(p, "encoder.mid_block.resnets.1", x, r)
+    x = silu(rms_norm(x, p["encoder.norm_out.gamma"], r), r)
+    x = causal_conv3d(x, p["encoder.conv_out.weight"], p["encoder.conv_out.bias"], 1, r)
+    x = causal_conv3d(x, p["quant_conv.weight"], p["quant_conv.bias"], 0, r)
+    mu = x[:, : cfg.z_dim]  # DiagonalGaussianDistribution.mode()
+    mean_t = torch.tensor(mean).view(1, -1, 1, 1, 1).to(BF16).float()
+    std_t = torch.tensor(std).view(1, -1, 1, 1, 1).to(BF16).float()
+    z = r(r(mu - mean_t) / std_t)
+    return pack_latents(z)

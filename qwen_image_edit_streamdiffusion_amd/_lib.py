@@ -71,6 +71,8 @@ SIGNATURES = {
     "qie_softmax_rows_f32_bf16": [P, L, P, L, I, I, F, P],
     "qie_transpose_bf16": [P, L, P, L, I, I, P],
     "qie_vae_rgb_out": [P, L, P, L, P],
+    "qie_vae_rgb_in": [P, P, L, P],
+    "qie_vae_latents_out_bf16": [P, L, I, I, I, P, P, P, P],
 }
 _RESTYPES = {"qie_strerror": c_char_p}
 

@@ -1141,9 +1141,10 @@ int launch_qkv_norm_rope(const void* x, int64_t ldx, const void* w, int M, int K
 struct ConvArgs {
   const bf16_t* in;
   int H_in, W_in, C;    // input image (NHWC), C % 8 == 0
-  int H_out, W_out;     // output image; == input, or 2x with up
-  int up;               // 1: nearest-2x upsample folded into the gather
-  int ks;               // 3 (pad 1) or 1
+  int H_out, W_out;     // output image
+  int mode;             // 0: same size (pad ks/2); 1: nearest-2x upsample folded into the gather;
+                        // 2: stride 2 after ZeroPad2d((0, 1, 0, 1)) (the encoder's Resample)
+  int ks;               // 3 or 1
 };
 __device__ __attribute__((aligned(16))) unsigned g_conv_zero[4];
 
@@ -1192,15 +1193,25 @@ __global__ void __launch_bounds__(WM * 2 * 64)
     for (int i = 0; i < PX; ++i) {
       const char* src = zero;
       if (tap[i] * c.C + ci[i] < kreal) {
-        int yy = py[i], xx = pxx[i];
+        int yy = py[i], xx = pxx[i], dy = 0, dx = 0;
         if (c.ks == 3) {
-          const int dy = (tap[i] * 11) >> 5;  // tap / 3 for tap < 9
-          yy += dy - 1;
-          xx += tap[i] - 3 * dy - 1;
+          dy = (tap[i] * 11) >> 5;  // tap / 3 for tap < 9
+          dx = tap[i] - 3 * dy;
         }
-        if (yy >= 0 && yy < c.H_out && xx >= 0 && xx < c.W_out) {
-          if (c.up) { yy >>= 1; xx >>= 1; }
-          src = (const char*)(c.in + ((int64_t)yy * c.W_in + xx) * c.C + ci[i]);
+        if (c.mode == 2) {  // stride 2, taps at 2y + dy (zero pad right / bottom)
+          yy = 2 * yy + dy;
+          xx = 2 * xx + dx;
+          if (yy < c.H_in && xx < c.W_in)
+            src = (const char*)(c.in + ((int64_t)yy * c.W_in + xx) * c.C + ci[i]);
+        } else {
+          if (c.ks == 3) {
+            yy += dy - 1;
+            xx += dx - 1;
+          }
+          if (yy >= 0 && yy < c.H_out && xx >= 0 && xx < c.W_out) {
+            if (c.mode == 1) { yy >>= 1; xx >>= 1; }
+            src = (const char*)(c.in + ((int64_t)yy * c.W_in + xx) * c.C + ci[i]);
+          }
         }
       }
       __builtin_amdgcn_global_load_lds((const void*)src, (QIE_LDS void*)(lds + (wave + i * NWAVE) * 1024), 16, 0, 0);
@@ -1446,15 +1457,18 @@ extern "C" int qie_linear_splitk_i8(const void* xq, int64_t ldx, const float* sx
 }
 
 // ---------------------------------------------------------------------------- VAE convolutions
-extern "C" int qie_conv2d_bf16(const void* x, int H_in, int W_in, int C, int up, int ksize, const void* w,
+extern "C" int qie_conv2d_bf16(const void* x, int H_in, int W_in, int C, int mode, int ksize, const void* w,
                                int64_t ldw, const void* bias, const void* resid, void* y, int N,
                                qie_stream_t stream) {
   QIE_CHECK_ARG(x && w && bias && y && H_in > 0 && W_in > 0 && C > 0 && C % 8 == 0);
-  QIE_CHECK_ARG((up == 0 || up == 1) && (ksize == 1 || ksize == 3) && N > 0 && N % 4 == 0);
+  QIE_CHECK_ARG(mode >= 0 && mode <= 2 && (ksize == 1 || ksize == 3) && N > 0 && N % 4 == 0);
+  QIE_CHECK_ARG(mode != 2 || (ksize == 3 && H_in % 2 == 0 && W_in % 2 == 0));
   const int kreal = ksize * ksize * C;
   const int kpad = (kreal + 63) / 64 * 64;
   QIE_CHECK_ARG(ldw >= kpad && ldw % 8 == 0 && ((uintptr_t)w % 16) == 0 && ((uintptr_t)x % 16) == 0);
-  ConvArgs c{(const bf16_t*)x, H_in, W_in, C, H_in << up, W_in << up, up, ksize};
+  const int H_out = mode == 1 ? 2 * H_in : mode == 2 ? H_in / 2 : H_in;
+  const int W_out = mode == 1 ? 2 * W_in : mode == 2 ? W_in / 2 : W_in;
+  ConvArgs c{(const bf16_t*)x, H_in, W_in, C, H_out, W_out, mode, ksize};
   const int64_t M64 = (int64_t)c.H_out * c.W_out;
   QIE_CHECK_ARG(M64 < (1ll << 31) && (int64_t)H_in * W_in * C < (1ll << 31));
   const int M = (int)M64;

@@ -170,6 +170,38 @@ __global__ void __launch_bounds__(256)
   }
 }
 
+// ---- image in (encoder): uint8 RGB [P][3] -> the image processor's bf16(2 (v / 255) - 1), NHWC
+// with the channels padded to 8 (zeros) for the conv gather's 16-byte chunks.
+__global__ void __launch_bounds__(256)
+    rgb_in_kernel(const uint8_t* __restrict__ rgb, bf16_t* __restrict__ y, int64_t P) {
+  const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (p >= P) return;
+  float v[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) v[c] = 2.0f * ((float)rgb[p * 3 + c] / 255.0f) - 1.0f;
+  *(u32x4_t*)(y + p * 8) = u32x4_t{pack2(v[0], v[1]), pack2(v[2], 0.f), 0u, 0u};
+}
+
+// ---- latents out (encoder): quant_conv output NHWC [B][h][w][ldx] -> mode (channels 0..15 = mu)
+// -> bf16(bf16(mu - mean) / std) -> packed [B][(h/2)(w/2)][64] (pipeline _encode_vae_image,
+// _pack_latents). One thread per packed element.
+__global__ void __launch_bounds__(256)
+    latents_out_kernel(const bf16_t* __restrict__ x, int64_t ldx, int B, int h, int w, const bf16_t* __restrict__ mean,
+                       const bf16_t* __restrict__ stdv, bf16_t* __restrict__ packed) {
+  const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t total = (int64_t)B * h * w * 16;
+  if (q >= total) return;
+  const int ch = (int)(q & 63);
+  const int64_t tok = q >> 6;
+  const int c = ch >> 2, dy = (ch >> 1) & 1, dx = ch & 1;
+  const int bi = (int)(tok / ((h / 2) * (w / 2)));
+  const int r = (int)(tok - (int64_t)bi * (h / 2) * (w / 2));
+  const int i = r / (w / 2), j = r - i * (w / 2);
+  const int64_t pix = ((int64_t)bi * h + 2 * i + dy) * w + 2 * j + dx;
+  const float mu = bf2f(x[pix * ldx + c]);
+  packed[q] = f2bf(rbf(mu - bf2f(mean[c])) / bf2f(stdv[c]));
+}
+
 }  // namespace
 
 extern "C" int qie_vae_latents_in_bf16(const void* packed, int batch, int h, int w, const void* sinv,
@@ -224,5 +256,22 @@ extern "C" int qie_vae_rgb_out(const void* x, int64_t ldx, void* rgb, int64_t pi
   QIE_CHECK_ARG(x && rgb && pixels > 0 && ldx >= 3);
   rgb_out_kernel<<<(unsigned)((pixels + 255) / 256), 256, 0, (hipStream_t)stream>>>((const bf16_t*)x, ldx,
                                                                                      (uint8_t*)rgb, pixels);
+  return qie_last_error();
+}
+
+extern "C" int qie_vae_rgb_in(const void* rgb, void* y, int64_t pixels, qie_stream_t stream) {
+  QIE_CHECK_ARG(rgb && y && pixels > 0 && ((uintptr_t)y % 16) == 0);
+  rgb_in_kernel<<<(unsigned)((pixels + 255) / 256), 256, 0, (hipStream_t)stream>>>((const uint8_t*)rgb, (bf16_t*)y,
+                                                                                    pixels);
+  return qie_last_error();
+}
+
+extern "C" int qie_vae_latents_out_bf16(const void* x, int64_t ldx, int batch, int h, int w, const void* mean,
+                                        const void* stdv, void* packed, qie_stream_t stream) {
+  QIE_CHECK_ARG(x && mean && stdv && packed && batch > 0 && h > 0 && w > 0 && h % 2 == 0 && w % 2 == 0);
+  QIE_CHECK_ARG(ldx >= 16);
+  const int64_t total = (int64_t)batch * h * w * 16;
+  latents_out_kernel<<<(unsigned)((total + 255) / 256), 256, 0, (hipStream_t)stream>>>(
+      (const bf16_t*)x, ldx, batch, h, w, (const bf16_t*)mean, (const bf16_t*)stdv, (bf16_t*)packed);
   return qie_last_error();
 }

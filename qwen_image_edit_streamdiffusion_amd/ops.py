@@ -437,10 +437,11 @@ def conv_kpad(C: int, ksize: int) -> int:
 
 
 def conv2d(x: torch.Tensor, H: int, W: int, w: torch.Tensor, b: torch.Tensor, ksize: int = 3, up: bool = False,
-           out: Optional[torch.Tensor] = None, residual: bool = False) -> torch.Tensor:
-    """NHWC conv (pad ksize//2) as an implicit GEMM: x [H*W, C] -> [H'*W', N] with H' = 2H when
-    ``up`` (nearest-2x folded into the gather). w [N, conv_kpad(C, ksize)] bf16. ``residual``:
-    ``out`` holds the shortcut and receives bf16(out + bf16(conv + b))."""
+           out: Optional[torch.Tensor] = None, residual: bool = False, down: bool = False) -> torch.Tensor:
+    """NHWC conv as an implicit GEMM: x [H*W, C] -> [H'*W', N]. Default pad ksize//2, H' = H; ``up``:
+    nearest-2x folded into the gather (H' = 2H); ``down``: stride 2 after ZeroPad2d((0,1,0,1))
+    (H' = H/2). w [N, conv_kpad(C, ksize)] bf16. ``residual``: ``out`` holds the shortcut and
+    receives bf16(out + bf16(conv + b))."""
     _dev(x, w, b, out)
     _chk(x.dtype == BF16 and w.dtype == BF16 and b.dtype == BF16, "bf16 operands required")
     _chk(x.dim() == 2 and x.is_contiguous() and x.shape[0] == H * W, "x: [H*W, C] contiguous")
@@ -448,12 +449,13 @@ def conv2d(x: torch.Tensor, H: int, W: int, w: torch.Tensor, b: torch.Tensor, ks
     N = w.shape[0]
     _chk(C % 8 == 0 and N % 4 == 0 and w.is_contiguous() and w.shape[1] >= conv_kpad(C, ksize), "conv shapes")
     _chk(b.numel() == N, "bias")
-    P = H * W * (4 if up else 1)
+    _chk(not (up and down) and (not down or (ksize == 3 and H % 2 == 0 and W % 2 == 0)), "conv mode")
+    P = H * W * 4 if up else (H // 2) * (W // 2) if down else H * W
     if out is None:
         _chk(not residual, "residual needs out")
         out = torch.empty(P, N, dtype=BF16, device=x.device)
     _chk(out.shape == (P, N) and out.is_contiguous() and out.dtype == BF16, "out [P, N]")
-    _lib.call("qie_conv2d_bf16", _p(x), H, W, C, int(up), ksize, _p(w), w.stride(0), _p(b),
+    _lib.call("qie_conv2d_bf16", _p(x), H, W, C, 1 if up else 2 if down else 0, ksize, _p(w), w.stride(0), _p(b),
               _p(out) if residual else None, _p(out), N, _stream())
     return out
 
@@ -530,4 +532,27 @@ def vae_rgb_out(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Te
         out = torch.empty(x.shape[0], 3, dtype=torch.uint8, device=x.device)
     _chk(out.shape == (x.shape[0], 3) and out.is_contiguous() and out.dtype == torch.uint8, "out")
     _lib.call("qie_vae_rgb_out", _p(x), x.stride(0), _p(out), x.shape[0], _stream())
+    return out
+
+
+def vae_rgb_in(rgb: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """uint8 RGB [P, 3] -> bf16 NHWC [P, 8] in [-1, 1] (channels 3..7 zero)."""
+    _dev(rgb, out)
+    _chk(rgb.dtype == torch.uint8 and rgb.dim() == 2 and rgb.shape[1] == 3 and rgb.is_contiguous(), "rgb [P, 3]")
+    if out is None:
+        out = torch.empty(rgb.shape[0], 8, dtype=BF16, device=rgb.device)
+    _chk(out.shape == (rgb.shape[0], 8) and out.is_contiguous() and out.dtype == BF16, "out [P, 8]")
+    _lib.call("qie_vae_rgb_in", _p(rgb), _p(out), rgb.shape[0], _stream())
+    return out
+
+
+def vae_latents_out(x: torch.Tensor, B: int, h: int, w: int, mean: torch.Tensor, std: torch.Tensor,
+                    out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """quant_conv output NHWC [B*h*w, >=16] -> normalised, packed latents [B, (h/2)(w/2), 64]."""
+    _dev(x, mean, std, out)
+    _chk(x.dtype == BF16 and _is2d_rowmajor(x) and x.shape[0] == B * h * w and x.shape[1] >= 16, "x")
+    if out is None:
+        out = torch.empty(B, h * w // 4, 64, dtype=BF16, device=x.device)
+    _chk(out.shape == (B, h * w // 4, 64) and out.is_contiguous(), "out")
+    _lib.call("qie_vae_latents_out_bf16", _p(x), x.stride(0), B, h, w, _p(mean), _p(std), _p(out), _stream())
     return out

@@ -31,7 +31,7 @@ import torch
 from . import ops
 from .scheduler import FlowMatchEulerDiscreteScheduler, calculate_shift, model_timesteps
 from .transformer import QwenImageTransformer2DModel
-from .vae import QwenImageVAEDecoder
+from .vae import QwenImageVAEDecoder, QwenImageVAEEncoder
 from . import weights as W
 
 BF16 = torch.bfloat16
@@ -66,6 +66,28 @@ def to_output(rgb: torch.Tensor, output_type: str):
     return [Image.fromarray(a) for a in arr]
 
 
+def images_to_rgb(image, device) -> torch.Tensor:
+    """The condition image(s) as uint8 RGB [n, H, W, 3] on the device at the VAE size: PIL images
+    are resized (LANCZOS) to calculate_dimensions(1024^2, aspect) as Edit-Plus does for its VAE
+    input; uint8 tensors [H, W, 3] / [n, H, W, 3] are taken as they are (H, W % 16 == 0)."""
+    if isinstance(image, torch.Tensor):
+        t = image if image.dim() == 4 else image[None]
+        if t.dtype != torch.uint8 or t.shape[-1] != 3:
+            raise ValueError("image tensors must be uint8 RGB [(n,) H, W, 3]")
+        return t.to(device).contiguous()
+    ims = image if isinstance(image, (list, tuple)) else [image]
+    if len(ims) != 1:
+        raise NotImplementedError("one condition image per prompt on the HIP encoder path")
+    import numpy as np
+    from PIL import Image
+    im = ims[0].convert("RGB")
+    w, h = calculate_dimensions(VAE_IMAGE_SIZE, im.size[0] / im.size[1])
+    w, h = w // 16 * 16, h // 16 * 16
+    if im.size != (w, h):
+        im = im.resize((w, h), Image.LANCZOS)
+    return torch.from_numpy(np.asarray(im).copy())[None].to(device)
+
+
 class QwenImageEditPlusPipeline:
     def __init__(self, transformer: QwenImageTransformer2DModel,
                  scheduler: Optional[FlowMatchEulerDiscreteScheduler] = None,
@@ -76,7 +98,8 @@ class QwenImageEditPlusPipeline:
         self.prompt_encoder = prompt_encoder
         self.image_encoder = image_encoder
         self.latent_decoder = latent_decoder
-        self.vae = None
+        self.vae = None          # QwenImageVAEDecoder (HIP): latents -> uint8 RGB
+        self.vae_encoder = None  # QwenImageVAEEncoder (HIP): condition image -> packed latents
         self.text_encoder = None
         self.vae_scale_factor = VAE_SCALE_FACTOR
         self._buf = {}
@@ -108,8 +131,10 @@ class QwenImageEditPlusPipeline:
         pipe = cls(model)
         if path is not None and W.find_vae_files(path):
             pipe.vae = W.load_vae_decoder(path, device=device)
+            pipe.vae_encoder = W.load_vae_encoder(path, device=device)
         elif random_init_seed is not None or path is None:
             pipe.vae = QwenImageVAEDecoder(device=device).random_init_(seed=(random_init_seed or 0) + 1)
+            pipe.vae_encoder = QwenImageVAEEncoder(device=device).random_init_(seed=(random_init_seed or 0) + 2)
         return pipe
 
     def to(self, device=None, *a, **k):
@@ -138,17 +163,24 @@ class QwenImageEditPlusPipeline:
         return embeds.to(BF16), mask
 
     def _image_latents(self, image, image_latents, B):
+        """Packed condition latents, and their (h, w) token grid when the HIP encoder made them."""
+        shape = None
         if image_latents is None:
-            if self.image_encoder is None:
+            if self.image_encoder is not None:
+                image_latents = self.image_encoder(image)
+            elif self.vae_encoder is not None:
+                rgb = images_to_rgb(image, self.transformer.device)
+                image_latents = self.vae_encoder.encode(rgb)
+                shape = (rgb.shape[1] // 16, rgb.shape[2] // 16)
+            else:
                 raise NotImplementedError(
-                    "VAE encoding (SURVEY.md §8 f1) is not on the HIP hot path yet: pass image_latents= "
-                    "(packed [B, S, 64]) or set pipe.image_encoder")
-            image_latents = self.image_encoder(image)
+                    "no VAE encoder: pass image_latents= (packed [B, S, 64]), set pipe.vae_encoder or "
+                    "pipe.image_encoder")
         if image_latents.dim() != 3:
             raise ValueError("image_latents must be packed [B, S, 64]")
         if image_latents.shape[0] == 1 and B > 1:
             image_latents = image_latents.expand(B, -1, -1)
-        return image_latents.to(BF16)
+        return image_latents.to(BF16), shape
 
     @staticmethod
     def prepare_noise(batch: int, height: int, width: int, generator: Optional[torch.Generator],
@@ -189,7 +221,9 @@ class QwenImageEditPlusPipeline:
             ne, nm = self._embeds(negative_prompt, image, negative_prompt_embeds, negative_prompt_embeds_mask)
             if ne.shape[0] != B:
                 ne, nm = ne.expand(B, -1, -1), nm.expand(B, -1)
-        cond = self._image_latents(image, image_latents, B)
+        cond, enc_shape = self._image_latents(image, image_latents, B)
+        if cond_shape is None and enc_shape is not None:
+            cond_shape = enc_shape
         if latents is None:
             latents = self.prepare_noise(B, height, width, generator, dev)
         S_noise = latents.shape[1]

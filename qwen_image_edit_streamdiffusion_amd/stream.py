@@ -228,6 +228,7 @@ class QwenRealtimePipeline:
         self.prompt_encoder = prompt_encoder
         self.latent_decoder = latent_decoder
         self.vae = None  # vae.QwenImageVAEDecoder: finished frames come out as uint8 RGB [H, W, 3]
+        self.vae_encoder = None  # vae.QwenImageVAEEncoder: uint8 RGB frames in
         self.generator: Optional[torch.Generator] = None
 
     def load_model(self, transformer: Optional[QwenImageTransformer2DModel] = None, seed: int = 0,
@@ -237,9 +238,13 @@ class QwenRealtimePipeline:
             transformer = QwenImageTransformer2DModel(**config_overrides).random_init_(seed)
         self.transformer = transformer
         if isinstance(vae, str) and vae == "random":
-            from .vae import QwenImageVAEDecoder
-            vae = QwenImageVAEDecoder(device=transformer.device).random_init_(seed + 1)
-        self.vae = vae
+            from .vae import QwenImageVAEDecoder, QwenImageVAEEncoder
+            vae = (QwenImageVAEDecoder(device=transformer.device).random_init_(seed + 1),
+                   QwenImageVAEEncoder(device=transformer.device).random_init_(seed + 2))
+        if isinstance(vae, tuple):
+            self.vae, self.vae_encoder = vae
+        else:
+            self.vae = vae
         self.generator = torch.Generator(device=transformer.device).manual_seed(42)
 
     def precompute_conditions(self, prompt: str, reference_image=None, prompt_embeds=None,
@@ -279,7 +284,15 @@ class QwenRealtimePipeline:
         """Push one frame (packed cond latents, or anything image_encoder accepts);
         return the latents of the frame that completed (None while filling)."""
         t0 = time.time()
-        cond = frame if isinstance(frame, torch.Tensor) else self.image_encoder(frame)
+        if isinstance(frame, torch.Tensor) and frame.dtype != torch.uint8:
+            cond = frame  # packed condition latents
+        elif self.image_encoder is not None:
+            cond = self.image_encoder(frame)
+        elif self.vae_encoder is not None:  # qwen_realtime.py:167-186 encode_image, on the HIP path
+            from .pipeline import images_to_rgb
+            cond = self.vae_encoder.encode(images_to_rgb(frame, self.transformer.device))
+        else:
+            raise NotImplementedError("frames must be packed latents, or set vae_encoder / image_encoder")
         noise = self.prepare_latent(cond)
         r = self.engine.push(noise, cond)
         self.frame_count += 1

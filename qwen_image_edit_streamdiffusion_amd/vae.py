@@ -107,12 +107,15 @@ def state_dict_shapes(cfg: VAEConfig) -> Dict[str, Tuple[int, ...]]:
     return s
 
 
-def conv_weight(w: torch.Tensor, n_pad: int = 0) -> torch.Tensor:
+def conv_weight(w: torch.Tensor, n_pad: int = 0, cin_pad: int = 0) -> torch.Tensor:
     """A causal conv3d [Cout, Cin, kt, k, k] / conv2d [Cout, Cin, k, k] weight as the
     [Cout (+n_pad)][conv_kpad] bf16 rows qie_conv2d_bf16 reads: the last temporal slice (the only
-    tap a first frame meets behind its causal zero padding), K order [ky][kx][Cin], zero padded."""
+    tap a first frame meets behind its causal zero padding), K order [ky][kx][Cin (+cin_pad zero
+    channels)], zero padded to a multiple of 64."""
     if w.dim() == 5:
         w = w[:, :, -1]
+    if cin_pad:
+        w = torch.cat([w, torch.zeros(w.shape[0], cin_pad, *w.shape[2:], dtype=w.dtype, device=w.device)], 1)
     co, ci, k, _ = w.shape
     rows = w.permute(0, 2, 3, 1).reshape(co, k * k * ci)
     out = torch.zeros(co + n_pad, ops.conv_kpad(ci, k), dtype=BF16, device=w.device)
@@ -120,97 +123,51 @@ def conv_weight(w: torch.Tensor, n_pad: int = 0) -> torch.Tensor:
     return out
 
 
-class QwenImageVAEDecoder:
-    """``vae.decode`` + pipeline decode tail on the HIP path. ``decode(packed, h, w)`` takes the
-    pipeline's packed latents [B, (h/2)(w/2), 64] (h, w in latent pixels) and returns uint8 RGB
-    [B, 8h, 8w, 3] on the device (``output="pt"``: the clamped bf16 image [B, 3, 8h, 8w])."""
+def _random_sd(shapes: Dict[str, Tuple[int, ...]], seed: int) -> Dict[str, torch.Tensor]:
+    """Random weights of the real architecture (fan-in scaled normal; gammas near 1)."""
+    g = torch.Generator().manual_seed(seed)
+    sd = {}
+    for name, shp in shapes.items():
+        if name.endswith("gamma"):
+            t = 1.0 + 0.05 * torch.randn(shp, generator=g)
+        elif name.endswith("bias"):
+            t = 0.02 * torch.randn(shp, generator=g)
+        else:
+            t = torch.randn(shp, generator=g) / math.sqrt(math.prod(shp[1:]))
+        sd[name] = t.to(BF16)
+    return sd
 
-    def __init__(self, config: Optional[VAEConfig] = None, device="cuda"):
-        self.config = config or VAEConfig()
-        self.device = torch.device(device)
-        if any(c % 8 for c in self.config.dims) or self.config.z_dim != 16:
-            raise NotImplementedError("the conv kernels need channel counts % 8 == 0 and z_dim 16")
-        self.w: Dict[str, torch.Tensor] = {}
-        self._ws: Dict[Tuple[int, int], Dict[str, torch.Tensor]] = {}
 
-    # ------------------------------------------------------------------ weights
-    def load_state_dict(self, sd: Dict[str, torch.Tensor], strict: bool = True) -> "QwenImageVAEDecoder":
-        """diffusers AutoencoderKLQwenImage state_dict (``decoder.*`` / ``post_quant_conv.*``; the
-        encoder half is ignored)."""
-        shapes = state_dict_shapes(self.config)
-        missing = [k for k in shapes if k not in sd]
-        if strict and missing:
-            raise KeyError(f"missing VAE decoder weights: {missing[:5]}{'...' if len(missing) > 5 else ''}")
-        dev = self.device
-        w = {}
-        for k, shp in shapes.items():
-            t = sd[k]
-            if tuple(t.shape) != shp:
-                raise ValueError(f"{k}: shape {tuple(t.shape)} != {shp}")
-            t = t.to(dev)
-            if k.endswith("gamma"):
-                w[k] = t.reshape(-1).to(BF16).contiguous()
-            elif k.endswith("bias"):
-                w[k] = t.to(BF16).contiguous()
-            elif "time_conv" in k:
-                continue  # first frame: time_conv is skipped upstream ("Rep" cache)
-            elif k in ("post_quant_conv.weight",):
-                w[k] = t.reshape(t.shape[0], t.shape[1]).to(BF16).contiguous()
-            elif t.dim() == 4 and t.shape[2:] == (1, 1) or t.dim() == 5 and t.shape[2:] == (1, 1, 1):
-                w[k] = conv_weight(t)  # 1x1 conv: K = Cin (padded to 64)
-            elif k == "decoder.conv_out.weight":
-                w[k] = conv_weight(t, n_pad=1)  # 3 -> 4 output channels (N % 4)
-            else:
-                w[k] = conv_weight(t)
-        w["decoder.conv_out.bias"] = torch.cat([w["decoder.conv_out.bias"], torch.zeros(1, dtype=BF16, device=dev)])
-        c = self.config
-        std = torch.tensor(c.latents_std, dtype=torch.float32).to(BF16)
-        w["sinv"] = (1.0 / std.float()).to(BF16).to(dev)  # 1.0 / bf16 tensor -> bf16 (pipeline)
-        w["mean"] = torch.tensor(c.latents_mean, dtype=torch.float32).to(BF16).to(dev)
-        self.w = w
-        return self
+def _convert(sd: Dict[str, torch.Tensor], shapes: Dict[str, Tuple[int, ...]], dev, strict: bool, what: str,
+             special: Dict[str, dict]) -> Dict[str, torch.Tensor]:
+    """Check names/shapes and convert a (de|en)coder state_dict to the kernel layouts: gammas and
+    biases flat bf16, convs to conv_weight rows (``special[name]`` = its extra kwargs), the
+    upsample3d / downsample3d time_conv dropped (never applied to a first frame)."""
+    missing = [k for k in shapes if k not in sd]
+    if strict and missing:
+        raise KeyError(f"missing VAE {what} weights: {missing[:5]}{'...' if len(missing) > 5 else ''}")
+    w = {}
+    for k, shp in shapes.items():
+        t = sd[k]
+        if tuple(t.shape) != shp:
+            raise ValueError(f"{k}: shape {tuple(t.shape)} != {shp}")
+        t = t.to(dev)
+        if k.endswith("gamma"):
+            w[k] = t.reshape(-1).to(BF16).contiguous()
+        elif k.endswith("bias"):
+            w[k] = t.to(BF16).contiguous()
+        elif "time_conv" in k:
+            continue
+        else:
+            w[k] = conv_weight(t, **special.get(k, {}))
+    return w
 
-    def random_init_(self, seed: int = 0) -> "QwenImageVAEDecoder":
-        """Random weights of the real architecture (fan-in scaled normal; gammas near 1)."""
-        g = torch.Generator().manual_seed(seed)
-        sd = {}
-        for name, shp in state_dict_shapes(self.config).items():
-            if name.endswith("gamma"):
-                t = 1.0 + 0.05 * torch.randn(shp, generator=g)
-            elif name.endswith("bias"):
-                t = 0.02 * torch.randn(shp, generator=g)
-            else:
-                t = torch.randn(shp, generator=g) / math.sqrt(math.prod(shp[1:]))
-            sd[name] = t.to(BF16)
-        return self.load_state_dict(sd)
 
-    # ------------------------------------------------------------------ workspace
-    def _workspace(self, h: int, w: int) -> Dict[str, torch.Tensor]:
-        key = (h, w)
-        if key not in self._ws:
-            c, dev = self.config, self.device
-            P0 = h * w
-            # activation buffers hold the largest pixels x channels of any stage
-            sizes, P = [P0 * c.dims[0]], P0
-            for a, b, mode in c.up_blocks():
-                sizes.append(P * max(a, b))
-                if mode is not None:
-                    P *= 4
-                    sizes.append(P * (b // 2))
-            n = max(sizes)
-            e = dict(dtype=BF16, device=dev)
-            C0 = c.dims[0]
-            self._ws[key] = {
-                "a": torch.empty(n, **e), "b": torch.empty(n, **e), "t": torch.empty(n, **e), "y": torch.empty(n, **e),
-                "z": torch.empty(P0, 16, **e), "qkv": torch.empty(P0, 3 * C0, **e),
-                # mid-block attention: K of P.V padded to 64 (zero P columns, zero V^T columns)
-                "s": torch.empty(P0, P0, dtype=torch.float32, device=dev),
-                "p": torch.empty(P0, -(-P0 // 64) * 64, **e),
-                "vt": torch.zeros(C0, -(-P0 // 64) * 64, **e), "att": torch.empty(P0, C0, **e),
-                "zero_b": torch.zeros(C0, **e),
-                "out": torch.empty(P, 4, **e),
-            }
-        return self._ws[key]
+class _VAEBlocks:
+    """The resnet / attention blocks both VAE halves share (NHWC, on the workspace buffers
+    "t", "y", "qkv", "s", "p", "vt", "att", "zero_b" and the free activation buffer named)."""
+
+    w: Dict[str, torch.Tensor]
 
     @staticmethod
     def _view(buf: torch.Tensor, P: int, C: int) -> torch.Tensor:
@@ -254,6 +211,73 @@ class QwenImageVAEDecoder:
         att = ws["att"][:P]
         ops.linear(p, vt, ws["zero_b"][:C], out=att)
         ops.conv2d(att, H, W, wt[f"{prefix}.proj.weight"], wt[f"{prefix}.proj.bias"], ksize=1, out=x, residual=True)
+
+
+    @staticmethod
+    def _attn_buffers(P0: int, C0: int, dev) -> Dict[str, torch.Tensor]:
+        """Mid-block attention over P0 tokens of C0 channels: K of P.V padded to 64 (zero P
+        columns from the softmax kernel, zero V^T columns here)."""
+        e = dict(dtype=BF16, device=dev)
+        kp = -(-P0 // 64) * 64
+        return {"qkv": torch.empty(P0, 3 * C0, **e), "s": torch.empty(P0, P0, dtype=torch.float32, device=dev),
+                "p": torch.empty(P0, kp, **e), "vt": torch.zeros(C0, kp, **e), "att": torch.empty(P0, C0, **e),
+                "zero_b": torch.zeros(C0, **e)}
+
+
+class QwenImageVAEDecoder(_VAEBlocks):
+    """``vae.decode`` + pipeline decode tail on the HIP path. ``decode(packed, h, w)`` takes the
+    pipeline's packed latents [B, (h/2)(w/2), 64] (h, w in latent pixels) and returns uint8 RGB
+    [B, 8h, 8w, 3] on the device (``output="pt"``: the clamped bf16 image [B, 3, 8h, 8w])."""
+
+    def __init__(self, config: Optional[VAEConfig] = None, device="cuda"):
+        self.config = config or VAEConfig()
+        self.device = torch.device(device)
+        if any(c % 8 for c in self.config.dims) or self.config.z_dim != 16:
+            raise NotImplementedError("the conv kernels need channel counts % 8 == 0 and z_dim 16")
+        self.w: Dict[str, torch.Tensor] = {}
+        self._ws: Dict[Tuple[int, int], Dict[str, torch.Tensor]] = {}
+
+    # ------------------------------------------------------------------ weights
+    def load_state_dict(self, sd: Dict[str, torch.Tensor], strict: bool = True) -> "QwenImageVAEDecoder":
+        """diffusers AutoencoderKLQwenImage state_dict (``decoder.*`` / ``post_quant_conv.*``; the
+        encoder half is ignored)."""
+        dev = self.device
+        w = _convert(sd, state_dict_shapes(self.config), dev, strict, "decoder",
+                     {"decoder.conv_out.weight": {"n_pad": 1}})  # 3 -> 4 output channels (N % 4)
+        pq = sd["post_quant_conv.weight"]
+        w["post_quant_conv.weight"] = pq.reshape(pq.shape[0], pq.shape[1]).to(dev).to(BF16).contiguous()
+        w["decoder.conv_out.bias"] = torch.cat([w["decoder.conv_out.bias"], torch.zeros(1, dtype=BF16, device=dev)])
+        c = self.config
+        std = torch.tensor(c.latents_std, dtype=torch.float32).to(BF16)
+        w["sinv"] = (1.0 / std.float()).to(BF16).to(dev)  # 1.0 / bf16 tensor -> bf16 (pipeline)
+        w["mean"] = torch.tensor(c.latents_mean, dtype=torch.float32).to(BF16).to(dev)
+        self.w = w
+        return self
+
+    def random_init_(self, seed: int = 0) -> "QwenImageVAEDecoder":
+        """Random weights of the real architecture (fan-in scaled normal; gammas near 1)."""
+        return self.load_state_dict(_random_sd(state_dict_shapes(self.config), seed))
+
+    # ------------------------------------------------------------------ workspace
+    def _workspace(self, h: int, w: int) -> Dict[str, torch.Tensor]:
+        key = (h, w)
+        if key not in self._ws:
+            c, dev = self.config, self.device
+            P0 = h * w
+            # activation buffers hold the largest pixels x channels of any stage
+            sizes, P = [P0 * c.dims[0]], P0
+            for a, b, mode in c.up_blocks():
+                sizes.append(P * max(a, b))
+                if mode is not None:
+                    P *= 4
+                    sizes.append(P * (b // 2))
+            n = max(sizes)
+            e = dict(dtype=BF16, device=dev)
+            C0 = c.dims[0]
+            self._ws[key] = {
+                "a": torch.empty(n, **e), "b": torch.empty(n, **e), "t": torch.empty(n, **e), "y": torch.empty(n, **e),
+                "z": torch.empty(P0, 16, **e), "out": torch.empty(P, 4, **e), **self._attn_buffers(P0, C0, dev)}
+        return self._ws[key]
 
     def decode(self, packed: torch.Tensor, h: int, w: int, output: str = "uint8") -> torch.Tensor:
         c, wt = self.config, self.w
@@ -321,3 +345,162 @@ class QwenImageVAEDecoder:
                 P *= 4
                 f += conv(b, b // 2, 3, P)
         return f + conv(d[-1], 3, 3, P)
+
+
+# ============================================================================ encoder (§8 f1)
+def encoder_plan(cfg: VAEConfig) -> List[Tuple]:
+    """QwenImageEncoder3d.down_blocks as a flat list (the diffusers ModuleList indices):
+    ("res", idx, in, out) and ("down", idx, C, mode)."""
+    dims = [cfg.base_dim * u for u in (1,) + tuple(cfg.dim_mult)]
+    plan, idx = [], 0
+    for i, (a, b) in enumerate(zip(dims[:-1], dims[1:])):
+        for _ in range(cfg.num_res_blocks):
+            plan.append(("res", idx, a, b))
+            idx += 1
+            a = b
+        if i != len(cfg.dim_mult) - 1:
+            plan.append(("down", idx, b, "downsample3d" if cfg.temperal_downsample[i] else "downsample2d"))
+            idx += 1
+    return plan
+
+
+def encoder_state_dict_shapes(cfg: VAEConfig) -> Dict[str, Tuple[int, ...]]:
+    """diffusers state_dict names/shapes of the encode path (``encoder.*``, ``quant_conv.*``)."""
+    z2 = 2 * cfg.z_dim
+    d0 = cfg.base_dim
+    s: Dict[str, Tuple[int, ...]] = {"encoder.conv_in.weight": (d0, 3, 3, 3, 3), "encoder.conv_in.bias": (d0,)}
+    top = d0
+    for op in encoder_plan(cfg):
+        if op[0] == "res":
+            s.update(_res_names(f"encoder.down_blocks.{op[1]}", op[2], op[3]))
+            top = op[3]
+        else:
+            u = f"encoder.down_blocks.{op[1]}"
+            s[f"{u}.resample.1.weight"] = (op[2], op[2], 3, 3)
+            s[f"{u}.resample.1.bias"] = (op[2],)
+            if op[3] == "downsample3d":
+                s[f"{u}.time_conv.weight"] = (op[2], op[2], 3, 1, 1)
+                s[f"{u}.time_conv.bias"] = (op[2],)
+    s.update(_res_names("encoder.mid_block.resnets.0", top, top))
+    s.update(_res_names("encoder.mid_block.resnets.1", top, top))
+    a = "encoder.mid_block.attentions.0"
+    s.update({f"{a}.norm.gamma": (top, 1, 1), f"{a}.to_qkv.weight": (3 * top, top, 1, 1),
+              f"{a}.to_qkv.bias": (3 * top,), f"{a}.proj.weight": (top, top, 1, 1), f"{a}.proj.bias": (top,)})
+    s.update({"encoder.norm_out.gamma": (top, 1, 1, 1), "encoder.conv_out.weight": (z2, top, 3, 3, 3),
+              "encoder.conv_out.bias": (z2,), "quant_conv.weight": (z2, z2, 1, 1, 1), "quant_conv.bias": (z2,)})
+    return s
+
+
+class QwenImageVAEEncoder(_VAEBlocks):
+    """``vae.encode`` + the pipeline's ``_encode_vae_image`` tail on the HIP path, one frame:
+    uint8 RGB [B, H, W, 3] (device) -> image processor normalisation -> QwenImageEncoder3d
+    (conv_in, down blocks with stride-2 Resamples folded into the conv gather, mid block,
+    RMS_norm + SiLU + conv_out) -> quant_conv -> DiagonalGaussian mode (mu) ->
+    ``(mu - mean) / std`` -> packed latents [B, (H/16)(W/16), 64] (SURVEY.md §8 a5 / f1;
+    the reference reaches it through QwenImageEditPlusPipeline.__call__ at server.py:137-153 and
+    the dead helper ``encode_image`` at qwen_realtime.py:167-186). The ``downsample3d`` time_conv
+    is skipped on a first frame, as upstream (its feat_cache starts empty)."""
+
+    def __init__(self, config: Optional[VAEConfig] = None, device="cuda"):
+        self.config = config or VAEConfig()
+        self.device = torch.device(device)
+        if self.config.base_dim % 8 or self.config.z_dim != 16:
+            raise NotImplementedError("the conv kernels need channel counts % 8 == 0 and z_dim 16")
+        self.w: Dict[str, torch.Tensor] = {}
+        self._ws: Dict[Tuple[int, int], Dict[str, torch.Tensor]] = {}
+
+    def load_state_dict(self, sd: Dict[str, torch.Tensor], strict: bool = True) -> "QwenImageVAEEncoder":
+        """diffusers AutoencoderKLQwenImage state_dict (``encoder.*`` / ``quant_conv.*``)."""
+        dev = self.device
+        w = _convert(sd, encoder_state_dict_shapes(self.config), dev, strict, "encoder",
+                     {"encoder.conv_in.weight": {"cin_pad": 5}})  # RGB -> 8 gathered channels
+        c = self.config
+        w["mean"] = torch.tensor(c.latents_mean, dtype=torch.float32).to(BF16).to(dev)
+        w["std"] = torch.tensor(c.latents_std, dtype=torch.float32).to(BF16).to(dev)
+        self.w = w
+        return self
+
+    def random_init_(self, seed: int = 0) -> "QwenImageVAEEncoder":
+        return self.load_state_dict(_random_sd(encoder_state_dict_shapes(self.config), seed))
+
+    def _workspace(self, H: int, W: int) -> Dict[str, torch.Tensor]:
+        key = (H, W)
+        if key not in self._ws:
+            c, dev = self.config, self.device
+            P, sizes, top = H * W, [H * W * 8], c.base_dim
+            for op in encoder_plan(c):
+                if op[0] == "res":
+                    sizes.append(P * max(op[2], op[3]))
+                    top = op[3]
+                else:
+                    P //= 4
+            e = dict(dtype=BF16, device=dev)
+            n = max(sizes + [H * W * c.base_dim])
+            self._ws[key] = {"a": torch.empty(n, **e), "b": torch.empty(n, **e), "t": torch.empty(n, **e),
+                             "y": torch.empty(n, **e), "rgb8": torch.empty(H * W, 8, **e),
+                             "zq": torch.empty(P, 2 * c.z_dim, **e), "zo": torch.empty(P, 2 * c.z_dim, **e),
+                             **self._attn_buffers(P, top, dev)}
+        return self._ws[key]
+
+    def encode(self, rgb: torch.Tensor) -> torch.Tensor:
+        """uint8 RGB [B, H, W, 3] on the device (H, W multiples of 16) -> packed latents."""
+        c, wt = self.config, self.w
+        if not wt:
+            raise RuntimeError("VAE encoder weights not loaded (load_state_dict / random_init_)")
+        B, H0, W0, _ = rgb.shape
+        if H0 % 16 or W0 % 16:
+            raise ValueError("image height and width must be multiples of 16")
+        ws = self._workspace(H0, W0)
+        outs = []
+        for bi in range(B):
+            x8 = ops.vae_rgb_in(rgb[bi].reshape(-1, 3).contiguous(), out=ws["rgb8"])
+            H, W, C = H0, W0, c.base_dim
+            cur, other = "a", "b"
+            x = self._view(ws[cur], H * W, C)
+            ops.conv2d(x8, H, W, wt["encoder.conv_in.weight"], wt["encoder.conv_in.bias"], out=x)
+            for op in encoder_plan(c):
+                if op[0] == "res":
+                    x, name = self._resnet(ws, f"encoder.down_blocks.{op[1]}", x, H, W, op[2], op[3], [other])
+                    if name is not None:
+                        cur, other = name, cur
+                    C = op[3]
+                else:
+                    u = f"encoder.down_blocks.{op[1]}.resample.1"
+                    nx = self._view(ws[other], (H // 2) * (W // 2), C)
+                    ops.conv2d(x, H, W, wt[f"{u}.weight"], wt[f"{u}.bias"], down=True, out=nx)
+                    cur, other = other, cur
+                    x = nx
+                    H, W = H // 2, W // 2
+            x, _ = self._resnet(ws, "encoder.mid_block.resnets.0", x, H, W, C, C, [other])
+            self._attention(ws, "encoder.mid_block.attentions.0", x, H, W, C)
+            x, _ = self._resnet(ws, "encoder.mid_block.resnets.1", x, H, W, C, C, [other])
+            t = self._view(ws["t"], H * W, C)
+            ops.vae_rms_norm(x, wt["encoder.norm_out.gamma"], True, out=t)
+            zo = ws["zo"]
+            ops.conv2d(t, H, W, wt["encoder.conv_out.weight"], wt["encoder.conv_out.bias"], out=zo)
+            zq = ws["zq"]
+            ops.conv2d(zo, H, W, wt["quant_conv.weight"], wt["quant_conv.bias"], ksize=1, out=zq)
+            outs.append(ops.vae_latents_out(zq, 1, H, W, wt["mean"], wt["std"]))
+        return torch.cat(outs)
+
+    def flops(self, H: int, W: int) -> float:
+        """Algorithmic FLOPs of one encode of an H x W image."""
+        c = self.config
+
+        def conv(ci, co, k, P):
+            return 2.0 * P * ci * co * k * k
+
+        P = H * W
+        f = conv(3, c.base_dim, 3, P)
+        top = c.base_dim
+        for op in encoder_plan(c):
+            if op[0] == "res":
+                a, b = op[2], op[3]
+                f += conv(a, b, 3, P) + conv(b, b, 3, P) + (conv(a, b, 1, P) if a != b else 0.0)
+                top = b
+            else:
+                P //= 4
+                f += conv(op[2], op[2], 3, P)
+        f += 2 * (2 * conv(top, top, 3, P)) + conv(top, 3 * top, 1, P) + 4.0 * P * P * top + conv(top, top, 1, P)
+        z2 = 2 * c.z_dim
+        return f + conv(top, z2, 3, P) + conv(z2, z2, 1, P)

@@ -190,12 +190,9 @@ def find_vae_files(path: str):
     return sorted(glob.glob(os.path.join(path, "vae", "*.safetensors"))) if os.path.isdir(path) else []
 
 
-def load_vae_decoder(path: str, device="cuda"):
-    """QwenImageVAEDecoder from a diffusers snapshot: ``vae/config.json`` (dims, latents_mean /
-    latents_std) and the decode half of the AutoencoderKLQwenImage state_dict (``decoder.*``,
-    ``post_quant_conv.*``; the encoder keys are skipped without being read)."""
+def _vae_config(path: str):
     import json
-    from .vae import QwenImageVAEDecoder, VAEConfig
+    from .vae import VAEConfig
     cfg = VAEConfig()
     cj = os.path.join(path, "vae", "config.json")
     if os.path.isfile(cj):
@@ -207,6 +204,10 @@ def load_vae_decoder(path: str, device="cuda"):
         for k in ("dim_mult", "temperal_downsample", "latents_mean", "latents_std"):
             if k in c:
                 setattr(cfg, k, tuple(c[k]))
+    return cfg
+
+
+def _vae_tensors(path: str, prefixes):
     files = find_vae_files(path)
     if not files:
         raise FileNotFoundError(f"no vae/*.safetensors under {path}")
@@ -215,6 +216,22 @@ def load_vae_decoder(path: str, device="cuda"):
     for f in files:
         with safe_open(f, framework="pt", device="cpu") as fh:
             for k in fh.keys():
-                if k.startswith("decoder.") or k.startswith("post_quant_conv."):
+                if k.startswith(prefixes):
                     sd[k] = fh.get_tensor(k)
-    return QwenImageVAEDecoder(cfg, device).load_state_dict(sd)
+    return sd
+
+
+def load_vae_decoder(path: str, device="cuda"):
+    """QwenImageVAEDecoder from a diffusers snapshot: ``vae/config.json`` (dims, latents_mean /
+    latents_std) and the decode half of the AutoencoderKLQwenImage state_dict (``decoder.*``,
+    ``post_quant_conv.*``; the other keys are skipped without being read)."""
+    from .vae import QwenImageVAEDecoder
+    return QwenImageVAEDecoder(_vae_config(path), device).load_state_dict(
+        _vae_tensors(path, ("decoder.", "post_quant_conv.")))
+
+
+def load_vae_encoder(path: str, device="cuda"):
+    """QwenImageVAEEncoder from the same snapshot (``encoder.*``, ``quant_conv.*``)."""
+    from .vae import QwenImageVAEEncoder
+    return QwenImageVAEEncoder(_vae_config(path), device).load_state_dict(
+        _vae_tensors(path, ("encoder.", "quant_conv.")))

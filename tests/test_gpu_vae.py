@@ -53,6 +53,8 @@ def _nhwc(x):  # [C, H, W] -> [H*W, C]
     (24, 20, 96, 4, 3, False),      # conv_out: 3 (+1 pad) channels, ragged tiles
     (128, 256, 64, 512, 3, False),  # 256-pixel tiles (8 waves): >= 512 workgroups
     (64, 128, 96, 384, 3, True),    # 256-pixel tiles through the upsampling gather
+    (32, 48, 96, 96, 3, "down"),    # encoder Resample: ZeroPad2d((0,1,0,1)) + stride 2
+    (256, 512, 64, 128, 3, "down"),  # stride 2 on 256-pixel tiles
 ])
 def test_conv2d(dev, H, W, C, N, k, up):
     from qwen_image_edit_streamdiffusion_amd.vae import conv_weight
@@ -60,11 +62,15 @@ def test_conv2d(dev, H, W, C, N, k, up):
     x = rnd((C, H, W), dev, 1.0, 1)
     w4 = rnd((N, C, k, k), dev, 1.0 / math.sqrt(C * k * k), 2)
     b = rnd((N,), dev, 0.1, 3)
-    y = ops.conv2d(_nhwc(x), H, W, conv_weight(w4), b, ksize=k, up=up)
+    down = up == "down"
+    y = ops.conv2d(_nhwc(x), H, W, conv_weight(w4), b, ksize=k, up=up is True, down=down)
     xi = x.float().cpu()[None]
-    if up:
-        xi = F.interpolate(xi, scale_factor=2.0, mode="nearest-exact")
-    ref = F.conv2d(xi, w4.float().cpu(), b.float().cpu(), padding=k // 2)[0].to(BF16)
+    if down:
+        ref = F.conv2d(F.pad(xi, (0, 1, 0, 1)), w4.float().cpu(), b.float().cpu(), stride=2)[0].to(BF16)
+    else:
+        if up:
+            xi = F.interpolate(xi, scale_factor=2.0, mode="nearest-exact")
+        ref = F.conv2d(xi, w4.float().cpu(), b.float().cpu(), padding=k // 2)[0].to(BF16)
     close(y, _nhwc(ref))
 
 
@@ -212,3 +218,67 @@ def test_pipeline_decodes_with_hip_vae(dev):
     assert np.array_equal(np.asarray(pil[0]), u8[0].cpu().numpy())
     pt = pipe(generator=torch.Generator().manual_seed(42), output_type="pt", **kw).images
     assert pt.shape == (1, 3, 128, 128) and torch.allclose(pt * 255, u8.permute(0, 3, 1, 2).float())
+
+
+def test_vae_rgb_in_latents_out(dev):
+    ops = _ops()
+    g = torch.Generator().manual_seed(20)
+    rgb = torch.randint(0, 256, (24 * 40, 3), generator=g, dtype=torch.uint8)
+    x = ops.vae_rgb_in(rgb.to(dev))
+    ref = (2.0 * (rgb.float() / 255.0) - 1.0).to(BF16)
+    assert torch.equal(x[:, :3].cpu(), ref) and (x[:, 3:] == 0).all()
+    z = rnd((2 * 16 * 24, 40), dev, 2.0, 21)  # quant_conv output, row stride 40 (>= 32)
+    mean = torch.tensor(V.LATENTS_MEAN).to(BF16)
+    std = torch.tensor(V.LATENTS_STD).to(BF16)
+    packed = ops.vae_latents_out(z, 2, 16, 24, mean.to(dev), std.to(dev))
+    mu = z[:, :16].cpu().float().view(2, 16, 24, 16).permute(0, 3, 1, 2)[:, :, None]
+    r = V._R(True)
+    want = V.pack_latents(r(r(mu - mean.float().view(1, -1, 1, 1, 1)) / std.float().view(1, -1, 1, 1, 1)))
+    assert torch.equal(packed.cpu().float(), want)
+
+
+def _small_encode(dev, seed=22):
+    from qwen_image_edit_streamdiffusion_amd.vae import QwenImageVAEEncoder, VAEConfig
+    enc = QwenImageVAEEncoder(VAEConfig(base_dim=16), dev).random_init_(9)
+    g = torch.Generator().manual_seed(seed)
+    rgb = torch.randint(0, 256, (1, 256, 256, 3), generator=g, dtype=torch.uint8)
+    p = V.random_encoder_params(V.VAEConfig(base_dim=16), 9)
+    return enc, rgb, p
+
+
+def test_vae_encode_vs_oracle(dev):
+    """Encoder (base_dim 16, 256x256 -> 32x32 latents, mid-block attention over 1024 tokens) vs
+    the oracle's causal-3-D restatement: rel-L2 <= 3e-2 on the normalised packed latents."""
+    enc, rgb, p = _small_encode(dev)
+    z = enc.encode(rgb.to(dev))
+    ref = V.encode(p, rgb, V.VAEConfig(base_dim=16), emulate_bf16=True)
+    assert z.shape == ref.shape == (1, 256, 64)
+    err = ((z.float().cpu() - ref).norm() / ref.norm()).item()
+    assert err <= 3e-2, err
+
+
+def test_pipeline_encodes_and_decodes_with_hip_vae(dev):
+    """pipe(image=PIL) with the HIP encoder == pipe(image_latents=encoder(image)); the image is
+    resized to the VAE size of its aspect ratio first."""
+    from PIL import Image
+    from oracle import dit_ref as R
+    from qwen_image_edit_streamdiffusion_amd import QwenImageEditPlusPipeline, QwenImageTransformer2DModel
+    from qwen_image_edit_streamdiffusion_amd.pipeline import images_to_rgb
+    from qwen_image_edit_streamdiffusion_amd.vae import QwenImageVAEDecoder, QwenImageVAEEncoder, VAEConfig
+    cfg = R.tiny_config()
+    m = QwenImageTransformer2DModel(num_layers=cfg.num_layers, num_attention_heads=cfg.num_attention_heads,
+                                    joint_attention_dim=cfg.joint_attention_dim, device=dev)
+    m.load_diffusers_state_dict(R.random_params(cfg, seed=0))
+    pipe = QwenImageEditPlusPipeline(m)
+    pipe.vae = QwenImageVAEDecoder(VAEConfig(base_dim=16), dev).random_init_(7)
+    pipe.vae_encoder = QwenImageVAEEncoder(VAEConfig(base_dim=16), dev).random_init_(8)
+    g = torch.Generator().manual_seed(23)
+    im = Image.fromarray(torch.randint(0, 256, (300, 300, 3), generator=g, dtype=torch.uint8).numpy())
+    pe = torch.randn(1, 20, cfg.joint_attention_dim, generator=g).to(BF16).to(dev)
+    rgb = images_to_rgb(im, dev)
+    assert rgb.shape == (1, 1024, 1024, 3)
+    kw = dict(prompt_embeds=pe, num_inference_steps=2, height=128, width=128, output_type="uint8")
+    a = pipe(image=im, generator=torch.Generator().manual_seed(42), **kw).images
+    lat = pipe.vae_encoder.encode(rgb)
+    b = pipe(image_latents=lat, cond_shape=(64, 64), generator=torch.Generator().manual_seed(42), **kw).images
+    assert a.shape == (1, 128, 128, 3) and torch.equal(a, b)

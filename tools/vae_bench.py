@@ -7,7 +7,7 @@ import time
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from qwen_image_edit_streamdiffusion_amd.vae import QwenImageVAEDecoder  # noqa: E402
+from qwen_image_edit_streamdiffusion_amd.vae import QwenImageVAEDecoder, QwenImageVAEEncoder  # noqa: E402
 
 
 def main():
@@ -29,6 +29,20 @@ def main():
     f = dec.flops(128, 128)
     print(f"vae decode 1024^2: {ms:.2f} ms  {f / ms / 1e9:.0f} TFLOP/s  img {tuple(img.shape)} "
           f"mean {img.float().mean().item():.1f}")
+    enc = QwenImageVAEEncoder(device=dev).random_init_(2)
+    rgb = img
+    for _ in range(2):
+        z = enc.encode(rgb)
+    torch.cuda.synchronize()
+    a.record()
+    for _ in range(n):
+        z = enc.encode(rgb)
+    b.record()
+    torch.cuda.synchronize()
+    ms = a.elapsed_time(b) / n
+    f = enc.flops(1024, 1024)
+    print(f"vae encode 1024^2: {ms:.2f} ms  {f / ms / 1e9:.0f} TFLOP/s  latents {tuple(z.shape)} "
+          f"std {z.float().std().item():.3f}")
 
 
 if __name__ == "__main__":
