@@ -8,14 +8,15 @@ of depth 2 (= the 2 Lightning steps), cond-only (the server's default
 use_cfg=False path, server.py:49,147-153), prompt-embed cache, 1024^2 output
 (4096 noise tokens) + 1024^2 condition image (4096 tokens) + 216 text tokens.
 One "step" = one pushed frame = one batched B=2 DiT forward + per-row Euler
-step, then the VAE decode of the frame that completed (HIP decoder, SURVEY.md
-§8 f1: unpack + de-normalise + post_quant_conv + QwenImageDecoder3d + uint8 RGB
-1024x1024x3 on the device; --no-decode leaves the latents); in steady state
-every step completes one image, so images/sec = completed frames / time.
-Synthetic inputs (randn with fixed seeds) are resident in HBM before the timed
-region.  The VAE encoder of the condition frame and the text encoder are not
-part of this path yet (the condition arrives as latents, the prompt embedding
-comes from the prompt cache).
+step, with the VAE on both ends (HIP): the pushed condition
+frame arrives as a uint8 RGB 1024x1024 camera image and is VAE-encoded
+(QwenImageEncoder3d + quant_conv + normalise + pack), and the frame that
+completes is VAE-decoded to uint8 RGB (unpack + de-normalise + post_quant_conv
++ QwenImageDecoder3d + postprocess).  --vae decode / none drop the encode /
+both.  In steady state every step completes one image, so images/sec =
+completed frames / time.  Synthetic inputs (randn / randint with fixed seeds)
+are resident in HBM before the timed region.  The text encoder is not on this
+path: the prompt embedding comes from the prompt cache.
 
 Multi-GPU (torch.distributed.run, one process per GPU, RCCL): each rank runs
 its own stream engine on its own frames (frame shard, weak scaling); rank 0
@@ -56,7 +57,7 @@ def log(*a):
         print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(decode: bool = True):
+def cpu_baseline(decode: bool = True, encode: bool = True):
     """Oracle (torch fp32 on the host cores) on a bounded sample of the SAME
     workload: one B=2 stream-batch forward with 1 of the 60 blocks (prologue +
     block + head) at full size, scaled x60 -> sec/image (1 forward/image)."""
@@ -86,6 +87,18 @@ def cpu_baseline(decode: bool = True):
         dv = (time.time() - t0) * V.decode_flops(vc, 128, 128) / V.decode_flops(vc, 32, 32)
         sec_per_image += dv
         sample += f" + VAE decode (256^2 sample, FLOP-scaled to 1024^2: {dv:.1f} s)"
+    if encode:  # VAE encode of a 256^2 frame, scaled by FLOPs to 1024^2
+        from oracle import vae_ref as V
+        vc = V.VAEConfig()
+        ep = V.random_encoder_params(vc, 2)
+        rgb = torch.randint(0, 256, (1, 256, 256, 3), generator=g, dtype=torch.uint8)
+        t0 = time.time()
+        V.encode(ep, rgb, vc, emulate_bf16=False)
+        from qwen_image_edit_streamdiffusion_amd.vae import QwenImageVAEEncoder, VAEConfig
+        ef = QwenImageVAEEncoder(VAEConfig(), "cpu")
+        de = (time.time() - t0) * ef.flops(1024, 1024) / ef.flops(256, 256)
+        sec_per_image += de
+        sample += f" + VAE encode (256^2 sample, FLOP-scaled: {de:.1f} s)"
     return {"value": 1.0 / sec_per_image, "unit": "images/sec", "cores": n, "kind": "port",
             "sample": sample + f" = {sec_per_image:.0f} s/image", "sec_per_image": sec_per_image}
 
@@ -113,8 +126,10 @@ def main():
     ap.add_argument("--workload", default="stream2", choices=["stream2", "stream2-int8", "stream2-cfg", "cfg4"])
     ap.add_argument("--layers", type=int, default=60, help="debug only; the headline needs 60")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-decode", action="store_true",
-                    help="stop at the finished latents (no VAE decode inside the timed step)")
+    ap.add_argument("--vae", default="both", choices=["both", "decode", "none"],
+                    help="VAE work inside the timed step: encode the uint8 RGB condition frame and decode "
+                         "the finished one (both, the default), decode only (condition frames arrive as "
+                         "latents), or none (DiT denoise alone)")
     ap.add_argument("--no-probe", action="store_true")
     ap.add_argument("--no-qk-fusion", action="store_true",
                     help="A/B: image QKV GEMM and QK RMSNorm+RoPE as two launches")
@@ -145,7 +160,7 @@ def main():
 
     from qwen_image_edit_streamdiffusion_amd import (QwenImageTransformer2DModel, StreamBatchDenoiser,
                                                      QwenImageEditPlusPipeline)
-    from qwen_image_edit_streamdiffusion_amd.vae import QwenImageVAEDecoder
+    from qwen_image_edit_streamdiffusion_amd.vae import QwenImageVAEDecoder, QwenImageVAEEncoder
     t_build = time.time()
     model = QwenImageTransformer2DModel(num_layers=args.layers, device=dev).random_init_(seed=0)
     if args.workload == "stream2-int8":
@@ -154,8 +169,10 @@ def main():
     model.fuse_qk_norm_rope = not args.no_qk_fusion
     model.log2q_attention = not args.no_log2q
     model.text_splits = args.text_splits or None
-    decode = not args.no_decode
+    decode = args.vae in ("both", "decode")
+    encode = args.vae == "both"
     vae = QwenImageVAEDecoder(device=dev).random_init_(seed=1) if decode else None
+    vae_enc = QwenImageVAEEncoder(device=dev).random_init_(seed=2) if encode else None
     torch.cuda.synchronize()
     log(f"[bench] model built in {time.time() - t_build:.1f}s, "
         f"{torch.cuda.memory_allocated() / 1e9:.1f} GB")
@@ -169,6 +186,9 @@ def main():
     nf = 8
     conds = [torch.randn(1, S_COND, 64, generator=gr, device=dev, dtype=BF16) for _ in range(nf)]
     noises = [torch.randn(1, S_NOISE, 64, generator=gr, device=dev, dtype=BF16) for _ in range(nf)]
+    if encode:  # condition frames as camera images: uint8 RGB 1024x1024, resident in HBM
+        frames = [torch.randint(0, 256, (1, 1024, 1024, 3), generator=gr, device=dev, dtype=torch.uint8)
+                  for _ in range(nf)]
 
     probe_keys = ("attention", "mlp_up")
     if args.workload.startswith("stream2"):
@@ -184,19 +204,20 @@ def main():
         fwd_per_step = 1
 
         def step(i):
-            return eng.push(noises[i % nf], conds[i % nf])
+            cond = vae_enc.encode(frames[i % nf]) if encode else conds[i % nf]
+            return eng.push(noises[i % nf], cond)
     else:  # cfg4: 4-step true-CFG 4.0, batched cond/uncond (B=2), one image per step
         pipe = QwenImageEditPlusPipeline(model)
         ne = torch.randn(1, 211, 3584, generator=g, device=dev, dtype=BF16)
         rows = 2
         fwd_per_step = 4
 
-        pipe.vae = vae
+        pipe.vae, pipe.vae_encoder = vae, vae_enc
 
         def step(i):
-            return pipe(prompt_embeds=pe, negative_prompt_embeds=ne, image_latents=conds[i % nf],
-                        latents=noises[i % nf], true_cfg_scale=4.0, num_inference_steps=4,
-                        output_type="uint8" if decode else "latent").images
+            src = dict(image=frames[i % nf]) if encode else dict(image_latents=conds[i % nf])
+            return pipe(prompt_embeds=pe, negative_prompt_embeds=ne, latents=noises[i % nf], true_cfg_scale=4.0,
+                        num_inference_steps=4, output_type="uint8" if decode else "latent", **src).images
 
     gather_buf = None
     if dist_on and rank == 0:
@@ -247,7 +268,8 @@ def main():
     sec_per_image = el * world / max(images, 1)
     S = S_NOISE + S_COND + S_TXT
     flops_fwd = model.flops_per_forward(S_NOISE + S_COND, S_TXT, B=rows)
-    flops_img = flops_fwd * fwd_per_step + (vae.flops(128, 128) if decode else 0.0)
+    flops_img = (flops_fwd * fwd_per_step + (vae.flops(128, 128) if decode else 0.0) +
+                 (vae_enc.flops(1024, 1024) if encode else 0.0))
     peak = PEAK_I8 if args.workload.endswith("int8") else PEAK_BF16
 
     kernels = {}
@@ -284,7 +306,7 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
-            cpu = cpu_baseline(decode)
+            cpu = cpu_baseline(decode, encode)
         except Exception as e:  # reported, never fatal to the GPU number
             cpu = {"error": repr(e)}
 
@@ -295,8 +317,8 @@ def main():
                     "stream2-cfg": "lightning-2step stream-batch depth=2 + true-CFG 4.0 (B=4), 1024x1024",
                     "cfg4": "4-step true-CFG 4.0 batched cond/uncond, 1024x1024 (configs[1])"}[args.workload]
         line = {
-            "metric": "images/sec, 1024x1024 2-step Lightning edit (DiT denoise" +
-                      (" + VAE decode)" if decode else ")"),
+            "metric": "images/sec, 1024x1024 2-step Lightning edit (" +
+                      ("VAE encode + " if encode else "") + "DiT denoise" + (" + VAE decode)" if decode else ")"),
             "value": value, "unit": "images/sec", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None,
@@ -305,7 +327,8 @@ def main():
                     "60-block architecture)",
             "config": {"workload": workload,
                        "model": "Qwen-Image-Edit-2509 DiT (60 blocks, D=3072)" +
-                                (" + AutoencoderKLQwenImage decoder" if decode else ""),
+                                (" + AutoencoderKLQwenImage " + ("encoder/decoder" if encode else "decoder")
+                                 if decode else ""),
                        "global_batch": rows * world, "seq_len": S, "layers": args.layers,
                        "parallelism": f"frame-shard x{world}" if world > 1 else "single"},
             "sec_per_image": sec_per_image,

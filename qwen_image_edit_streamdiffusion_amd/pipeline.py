@@ -206,8 +206,10 @@ class QwenImageEditPlusPipeline:
         # guidance_scale is a no-op for this non-guidance-distilled model [U]
         dev = self.transformer.device
         if height is None or width is None:
-            if image is not None and hasattr(image[-1] if isinstance(image, list) else image, "size"):
-                im = image[-1] if isinstance(image, list) else image
+            im = image[-1] if isinstance(image, list) else image
+            if isinstance(im, torch.Tensor):  # uint8 RGB [(n,) H, W, 3]
+                width, height = calculate_dimensions(VAE_IMAGE_SIZE, im.shape[-2] / im.shape[-3])
+            elif im is not None and hasattr(im, "size"):
                 width, height = calculate_dimensions(VAE_IMAGE_SIZE, im.size[0] / im.size[1])
             else:
                 width, height = 1024, 1024
