@@ -9,6 +9,7 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 900 python bench.py --steps 10 --warmup 3 > $OUT/bench.json 2> $OUT/bench.err || exit 1
 echo "bench: $(cat $OUT/bench.json | head -c 300)"
+timeout -k 10 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --vae none > $OUT/bench_dit.json 2> $OUT/bench_dit.err || exit 1
 timeout -k 10 600 python bench.py --steps 6 --warmup 2 --no-cpu-baseline --workload stream2-int8 > $OUT/bench_int8.json 2> $OUT/bench_int8.err || exit 1
 timeout -k 10 600 python bench.py --steps 6 --warmup 2 --no-cpu-baseline --workload stream2-cfg > $OUT/bench_stream2cfg.json 2> $OUT/bench_stream2cfg.err || exit 1
 timeout -k 10 600 python bench.py --steps 3 --warmup 1 --no-cpu-baseline --workload cfg4 > $OUT/bench_cfg4.json 2> $OUT/bench_cfg4.err || exit 1

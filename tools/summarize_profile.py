@@ -31,7 +31,7 @@ def main():
     dst = os.path.join(ROOT, "profiles")
     os.makedirs(dst, exist_ok=True)
     shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(dst, f"{tag}_kernel_stats.csv"))
-    for f in ("bench", "bench_int8", "bench_cfg4", "bench_stream2cfg"):
+    for f in ("bench", "bench_dit", "bench_int8", "bench_cfg4", "bench_stream2cfg"):
         p = os.path.join(src, f + ".json")
         if os.path.exists(p):
             shutil.copy(p, os.path.join(dst, f"{tag}_{f}.json"))
