@@ -1148,11 +1148,12 @@ struct ConvArgs {
 };
 __device__ __attribute__((aligned(16))) unsigned g_conv_zero[4];
 
-template <int EPI, int BM, int WM>
+template <int EPI, int BM, int WM, int BN, int MODE>
 __global__ void __launch_bounds__(WM * 2 * 64)
     conv_kernel(ConvArgs c, const char* __restrict__ W, int64_t ldw_b, int M, int N, int K_bytes, EpiArgs e) {
   using Op = MfmaOp<false>;
-  constexpr int BN = 128, WN = 2, NWAVE = WM * WN;
+  constexpr int WN = 2, NWAVE = WM * WN;
+  constexpr int WPC = BN / 8;  // W pieces (8 rows x 128 B) per K tile, spread over the waves
   constexpr int TM = BM / WM, TN = BN / WN, MT = TM / 16, NTL = TN / 16;
   constexpr int A_BYTES = BM * kRowBytes, W_BYTES = BN * kRowBytes, STAGE = A_BYTES + W_BYTES;
   constexpr int PX = BM / 8 / NWAVE;  // X pieces per lane per K tile
@@ -1169,14 +1170,14 @@ __global__ void __launch_bounds__(WM * 2 * 64)
   const int tm = first_m + (wgid % per_group) % gsz;
   const int tn = (wgid % per_group) / gsz;
   const int m0 = tm * BM, n0 = tn * BN;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  // wave index made provably uniform: the LDS-DMA destination (M0) must be, or hipcc waterfalls
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int wm = wave / WN, wn = wave % WN;
   const char* wg = W + (int64_t)n0 * ldw_b;
   const int n_valid = N - n0;
 
   // per X piece: output pixel (y, x) of its row, and the (tap, channel) of its chunk in the K tile
   int py[PX], pxx[PX], tap[PX], ci[PX];
-  const int kreal = c.ks * c.ks * c.C;
 #pragma unroll
   for (int i = 0; i < PX; ++i) {
     const int r = (wave + i * NWAVE) * 8 + (lane >> 3);
@@ -1187,37 +1188,42 @@ __global__ void __launch_bounds__(WM * 2 * 64)
     tap[i] = k / c.C;
     ci[i] = k - tap[i] * c.C;
   }
+  const int ntap = c.ks * c.ks, pad = c.ks >> 1;
+  const int hlim = MODE == 2 ? c.H_in : c.H_out, wlim = MODE == 2 ? c.W_in : c.W_out;
   const char* zero = (const char*)g_conv_zero;
-  auto stage_x = [&](int kt, char QIE_LDS* lds) {
+  // branch-free gather: the chunk's source pixel for its tap, or the zero chunk
+  auto stage_x = [&](char QIE_LDS* lds) {
 #pragma unroll
     for (int i = 0; i < PX; ++i) {
-      const char* src = zero;
-      if (tap[i] * c.C + ci[i] < kreal) {
-        int yy = py[i], xx = pxx[i], dy = 0, dx = 0;
-        if (c.ks == 3) {
-          dy = (tap[i] * 11) >> 5;  // tap / 3 for tap < 9
-          dx = tap[i] - 3 * dy;
-        }
-        if (c.mode == 2) {  // stride 2, taps at 2y + dy (zero pad right / bottom)
-          yy = 2 * yy + dy;
-          xx = 2 * xx + dx;
-          if (yy < c.H_in && xx < c.W_in)
-            src = (const char*)(c.in + ((int64_t)yy * c.W_in + xx) * c.C + ci[i]);
-        } else {
-          if (c.ks == 3) {
-            yy += dy - 1;
-            xx += dx - 1;
-          }
-          if (yy >= 0 && yy < c.H_out && xx >= 0 && xx < c.W_out) {
-            if (c.mode == 1) { yy >>= 1; xx >>= 1; }
-            src = (const char*)(c.in + ((int64_t)yy * c.W_in + xx) * c.C + ci[i]);
-          }
-        }
+      const int t = tap[i];
+      const int dy = (t * 11) >> 5, dx = t - 3 * dy;  // tap / 3, tap % 3 for tap < 9 (0, 0 for 1x1)
+      int yy, xx;
+      if constexpr (MODE == 2) {  // stride 2 after ZeroPad2d((0, 1, 0, 1))
+        yy = 2 * py[i] + dy;
+        xx = 2 * pxx[i] + dx;
+      } else {
+        yy = py[i] + dy - pad;
+        xx = pxx[i] + dx - pad;
       }
+      const bool ok = t < ntap && yy >= 0 && xx >= 0 && yy < hlim && xx < wlim;
+      if constexpr (MODE == 1) {  // nearest-2x: the upsampled pixel's source
+        yy >>= 1;
+        xx >>= 1;
+      }
+      // 32-bit element offset (the host checks H_in * W_in * C < 2^31)
+      const char* src = ok ? (const char*)c.in + 2u * (uint32_t)((yy * c.W_in + xx) * c.C + ci[i]) : zero;
       __builtin_amdgcn_global_load_lds((const void*)src, (QIE_LDS void*)(lds + (wave + i * NWAVE) * 1024), 16, 0, 0);
       // advance to the next K tile: 64 channels on, wrapping into the following taps
       ci[i] += 64;
-      while (ci[i] >= c.C) { ci[i] -= c.C; ++tap[i]; }
+      if (c.C >= 64) {
+        const int wr = ci[i] >= c.C;
+        ci[i] -= wr * c.C;
+        tap[i] += wr;
+      } else {
+        const int q = ci[i] / c.C;
+        ci[i] -= q * c.C;
+        tap[i] += q;
+      }
     }
   };
 
@@ -1228,8 +1234,22 @@ __global__ void __launch_bounds__(WM * 2 * 64)
     for (int j = 0; j < NTL; ++j) acc[i][j] = typename Op::acc{0, 0, 0, 0};
 
   const int nk = K_bytes / kRowBytes;
-  stage_x(0, smem);
-  stage_tile<BN, NWAVE>(wg, ldw_b, n_valid, smem + A_BYTES, wave, lane);
+  // W rows: piece q (rows 8q..8q+7) by wave q % NWAVE; BN = 96 leaves some waves one piece short
+  auto stage_w = [&](int64_t koff, char QIE_LDS* lds) {
+#pragma unroll
+    for (int i = 0; i < (WPC + NWAVE - 1) / NWAVE; ++i) {
+      const int blk = wave + i * NWAVE;
+      if (WPC % NWAVE == 0 || blk < WPC) {
+        const int r = blk * 8 + (lane >> 3);
+        const int cc = swz_chunk(r, lane & 7);
+        const int gr = r < n_valid ? r : n_valid - 1;
+        __builtin_amdgcn_global_load_lds((const void*)(wg + (int64_t)gr * ldw_b + koff + (cc << 4)),
+                                         (QIE_LDS void*)(lds + blk * 1024), 16, 0, 0);
+      }
+    }
+  };
+  stage_x(smem);
+  stage_w(0, smem + A_BYTES);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   const int fr = lane & 15;
@@ -1240,8 +1260,8 @@ __global__ void __launch_bounds__(WM * 2 * 64)
     const int cur = kt & 1;
     if (kt + 1 < nk) {
       char QIE_LDS* nb = smem + (cur ^ 1) * STAGE;
-      stage_x(kt + 1, nb);
-      stage_tile<BN, NWAVE>(wg + (int64_t)(kt + 1) * kRowBytes, ldw_b, n_valid, nb + A_BYTES, wave, lane);
+      stage_x(nb);
+      stage_w((int64_t)(kt + 1) * kRowBytes, nb + A_BYTES);
     }
     const char QIE_LDS* at = smem + cur * STAGE;
     const char QIE_LDS* wt = at + A_BYTES;
@@ -1476,16 +1496,36 @@ extern "C" int qie_conv2d_bf16(const void* x, int H_in, int W_in, int C, int mod
   QIE_CHECK_ARG(!resid || resid == y);  // y = bf16(resid + bf16(acc + bias)), in place
   EpiArgs e = make_epi(y, N, bias);
   const char* wc = (const char*)w;
-  // 256-pixel tiles (8 waves) once they still give >= 2 workgroups per CU, else 128 (4 waves)
-  const int tn = (N + 127) / 128;
+  // 256-pixel tiles (8 waves) once they still give >= 2 workgroups per CU, else 128 (4 waves);
+  // 96-wide output tiles when N is a multiple of 96 but not of 128 (96, 192: no idle columns)
+  const bool n96 = N % 128 != 0 && N % 96 == 0;
+  const int bn = n96 ? 96 : 128;
+  const int tn = (N + bn - 1) / bn;
   const int64_t big = (int64_t)((M + 255) / 256) * tn;
+  const int64_t kb = kpad * 2, lw = ldw * 2;
+  auto go = [&](auto bm_t, auto wm_t, auto bn_t) {
+    constexpr int BM = decltype(bm_t)::value, WMv = decltype(wm_t)::value, BNv = decltype(bn_t)::value;
+    const int nwg = ((M + BM - 1) / BM) * ((N + BNv - 1) / BNv);
+    auto k = [&](auto mode_t) {
+      constexpr int MD = decltype(mode_t)::value;
+      if (resid) conv_kernel<EPI_RES, BM, WMv, BNv, MD><<<nwg, WMv * 128, 0, s>>>(c, wc, lw, M, N, (int)kb, e);
+      else conv_kernel<EPI_BIAS, BM, WMv, BNv, MD><<<nwg, WMv * 128, 0, s>>>(c, wc, lw, M, N, (int)kb, e);
+    };
+    if (mode == 1) k(std::integral_constant<int, 1>{});
+    else if (mode == 2) k(std::integral_constant<int, 2>{});
+    else k(std::integral_constant<int, 0>{});
+  };
+  using I96 = std::integral_constant<int, 96>;
+  using I128 = std::integral_constant<int, 128>;
+  using I256 = std::integral_constant<int, 256>;
+  using I2 = std::integral_constant<int, 2>;
+  using I4 = std::integral_constant<int, 4>;
   if (big >= 512) {
-    if (resid) conv_kernel<EPI_RES, 256, 4><<<(int)big, 512, 0, s>>>(c, wc, ldw * 2, M, N, kpad * 2, e);
-    else conv_kernel<EPI_BIAS, 256, 4><<<(int)big, 512, 0, s>>>(c, wc, ldw * 2, M, N, kpad * 2, e);
+    if (n96) go(I256{}, I4{}, I96{});
+    else go(I256{}, I4{}, I128{});
   } else {
-    const int nwg = ((M + 127) / 128) * tn;
-    if (resid) conv_kernel<EPI_RES, 128, 2><<<nwg, 256, 0, s>>>(c, wc, ldw * 2, M, N, kpad * 2, e);
-    else conv_kernel<EPI_BIAS, 128, 2><<<nwg, 256, 0, s>>>(c, wc, ldw * 2, M, N, kpad * 2, e);
+    if (n96) go(I128{}, I2{}, I96{});
+    else go(I128{}, I2{}, I128{});
   }
   return qie_last_error();
 }
