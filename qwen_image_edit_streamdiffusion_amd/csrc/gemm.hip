@@ -1147,6 +1147,16 @@ struct ConvArgs {
   int ks;               // 3 or 1
 };
 __device__ __attribute__((aligned(16))) unsigned g_conv_zero[4];
+// Tile choice, measured (tools/conv_bench.py, same-process A/B on the VAE shapes): with the
+// branch-free gather, 128-pixel tiles at 2 workgroups per CU beat 256-pixel tiles at 1 per CU by
+// 3-11 %, and a 3-stage LDS ring (two K tiles in flight) loses 2-4 % (and 40 % where it halves
+// the workgroups per CU). Both remain build options.
+#ifndef QIE_CONV_BIG_MIN  // workgroup count of 256-pixel tiles from which they replace 128-pixel ones
+#define QIE_CONV_BIG_MIN (1 << 30)
+#endif
+#ifndef QIE_CONV_STAGES  // 2: double-buffered K tiles, drain each step; 3: two tiles in flight
+#define QIE_CONV_STAGES 2
+#endif
 
 template <int EPI, int BM, int WM, int BN, int MODE>
 __global__ void __launch_bounds__(WM * 2 * 64)
@@ -1157,7 +1167,8 @@ __global__ void __launch_bounds__(WM * 2 * 64)
   constexpr int TM = BM / WM, TN = BN / WN, MT = TM / 16, NTL = TN / 16;
   constexpr int A_BYTES = BM * kRowBytes, W_BYTES = BN * kRowBytes, STAGE = A_BYTES + W_BYTES;
   constexpr int PX = BM / 8 / NWAVE;  // X pieces per lane per K tile
-  __shared__ __attribute__((aligned(16))) char smem_raw[2 * STAGE];
+  constexpr int NS = QIE_CONV_STAGES;  // LDS stages: tile kt + NS - 1 is in flight while kt computes
+  __shared__ __attribute__((aligned(16))) char smem_raw[NS * STAGE];
   char QIE_LDS* smem = (char QIE_LDS*)smem_raw;
 
   const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
@@ -1248,20 +1259,42 @@ __global__ void __launch_bounds__(WM * 2 * 64)
       }
     }
   };
+  // loads one K tile puts in flight per wave (vmcnt counts them): PX gather pieces + this wave's W
+  const int nw_mine = WPC / NWAVE + (wave < WPC % NWAVE ? 1 : 0);
+  auto wait_newest_in_flight = [&](int n) {  // vmcnt(n): all but this wave's n newest loads landed
+    switch (n) {
+      case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+      case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+      case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+      case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+      default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    }
+  };
   stage_x(smem);
   stage_w(0, smem + A_BYTES);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if constexpr (NS == 3) {
+    if (nk > 1) {
+      stage_x(smem + STAGE);
+      stage_w(kRowBytes, smem + STAGE + A_BYTES);
+      wait_newest_in_flight(PX + nw_mine);
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
   __syncthreads();
   const int fr = lane & 15;
   const int sw = (fr >> 1) & 7;
   const int a_row = wm * TM + fr;
   const int w_row = wn * TN + fr;
   for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) {
-      char QIE_LDS* nb = smem + (cur ^ 1) * STAGE;
+    const int cur = kt % NS;
+    const bool more = kt + NS - 1 < nk;
+    if (more) {
+      char QIE_LDS* nb = smem + ((kt + NS - 1) % NS) * STAGE;
       stage_x(nb);
-      stage_w((int64_t)(kt + 1) * kRowBytes, nb + A_BYTES);
+      stage_w((int64_t)(kt + NS - 1) * kRowBytes, nb + A_BYTES);
     }
     const char QIE_LDS* at = smem + cur * STAGE;
     const char QIE_LDS* wt = at + A_BYTES;
@@ -1278,7 +1311,9 @@ __global__ void __launch_bounds__(WM * 2 * 64)
 #pragma unroll
         for (int j = 0; j < NTL; ++j) acc[i][j] = Op::mma(wf[j], af[i], acc[i][j]);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // tile kt+1 must have landed: NS = 3 leaves tile kt+2's loads (issued above) in flight
+    if (NS == 3 && more) wait_newest_in_flight(PX + nw_mine);
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
 #pragma unroll
@@ -1496,8 +1531,8 @@ extern "C" int qie_conv2d_bf16(const void* x, int H_in, int W_in, int C, int mod
   QIE_CHECK_ARG(!resid || resid == y);  // y = bf16(resid + bf16(acc + bias)), in place
   EpiArgs e = make_epi(y, N, bias);
   const char* wc = (const char*)w;
-  // 256-pixel tiles (8 waves) once they still give >= 2 workgroups per CU, else 128 (4 waves);
-  // 96-wide output tiles when N is a multiple of 96 but not of 128 (96, 192: no idle columns)
+  // 128-pixel tiles (4 waves, 2 workgroups per CU; 256-pixel / 8-wave tiles from QIE_CONV_BIG_MIN
+  // workgroups); 96-wide output tiles when N is a multiple of 96 but not of 128 (96, 192)
   const bool n96 = N % 128 != 0 && N % 96 == 0;
   const int bn = n96 ? 96 : 128;
   const int tn = (N + bn - 1) / bn;
@@ -1520,7 +1555,7 @@ extern "C" int qie_conv2d_bf16(const void* x, int H_in, int W_in, int C, int mod
   using I256 = std::integral_constant<int, 256>;
   using I2 = std::integral_constant<int, 2>;
   using I4 = std::integral_constant<int, 4>;
-  if (big >= 512) {
+  if (big >= QIE_CONV_BIG_MIN) {
     if (n96) go(I256{}, I4{}, I96{});
     else go(I256{}, I4{}, I128{});
   } else {

@@ -51,12 +51,12 @@ def _nhwc(x):  # [C, H, W] -> [H*W, C]
     (8, 16, 384, 192, 3, True),     # Resample: upsample folded into the gather
     (16, 16, 192, 384, 1, False),   # conv_shortcut 1x1
     (24, 20, 96, 4, 3, False),      # conv_out: 3 (+1 pad) channels, ragged tiles
-    (128, 256, 64, 512, 3, False),  # 256-pixel tiles (8 waves): >= 512 workgroups
-    (64, 128, 96, 384, 3, True),    # 256-pixel tiles through the upsampling gather
+    (128, 256, 64, 512, 3, False),  # many workgroups
+    (64, 128, 96, 384, 3, True),    # upsampling gather, 2 workgroups per CU
     (32, 48, 96, 96, 3, "down"),    # encoder Resample: ZeroPad2d((0,1,0,1)) + stride 2
-    (256, 512, 64, 128, 3, "down"),  # stride 2 on 256-pixel tiles
-    (256, 256, 64, 192, 3, False),  # 96-wide output tiles, 256-pixel tiles
-    (256, 512, 32, 96, 3, False),   # N = 96 on 256-pixel tiles (C = 32 < 64: multi-tap K tiles)
+    (256, 512, 64, 128, 3, "down"),  # stride 2, many workgroups
+    (256, 256, 64, 192, 3, False),  # 96-wide output tiles
+    (256, 512, 32, 96, 3, False),   # N = 96, C = 32 < 64: multi-tap K tiles
 ])
 def test_conv2d(dev, H, W, C, N, k, up):
     from qwen_image_edit_streamdiffusion_amd.vae import conv_weight
