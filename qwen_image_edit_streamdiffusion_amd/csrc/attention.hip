@@ -64,6 +64,12 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 // the end of an M-phase (this wave's pieces from its previous V-phase), vmcnt(pieces) at the
 // end of a V-phase; one barrier per phase.
 constexpr int kRing = 3;
+#ifndef QIE_ATTN_MPRIO  // issue priority of a wave in its MFMA phase
+#define QIE_ATTN_MPRIO 2
+#endif
+#ifndef QIE_ATTN_VPRIO  // ... and in its softmax phase
+#define QIE_ATTN_VPRIO 0
+#endif
 #ifndef QIE_ATTN_ABL  // diagnostic ablations (wrong results): 1 no K/V DMA in the loop, 2 no exp2
 #define QIE_ATTN_ABL 0
 #endif
@@ -247,7 +253,7 @@ __global__ void __launch_bounds__(512) attn_pp_kernel(AttnArgs a) {
     bf16x8_t A[8];
     // the MFMA wave outranks its SIMD partner (in its softmax phase) for issue: otherwise the
     // older wave group wins arbitration and starves the younger group's MFMA phase
-    __builtin_amdgcn_s_setprio(2);
+    __builtin_amdgcn_s_setprio(QIE_ATTN_MPRIO);
 #pragma unroll
     for (int i = i0; i < i0 + PF && i < i1; ++i) A[i & 7] = opA(i, tk, tv);
 #pragma unroll
@@ -255,7 +261,7 @@ __global__ void __launch_bounds__(512) attn_pp_kernel(AttnArgs a) {
       if (i + PF < i1) A[(i + PF) & 7] = opA(i + PF, tk, tv);
       mfma_i(i, A[i & 7]);
     }
-    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_setprio(QIE_ATTN_VPRIO);
   };
   // V-phase: softmax of S(t) into P(t), DMA of later tiles; ends with the phase barrier
   auto vphase = [&](int t) {

@@ -49,5 +49,31 @@ int main() {
     printf("group %d: tiles %.0f  M-body %.0f  M-end wait+barrier %.0f  V-phase %.0f  cycles/tile (s_memtime)\n",
            g, nt, st[g][0] / nt, st[g][1] / nt, st[g][2] / nt);
   }
+  // the model's path: q pre-scaled by scale * log2(e), qie_attention_fwd_log2q_bf16
+  const size_t qn = (size_t)B * H * s_pad * 128;
+  for (size_t i = 0; i < qn; ++i) {
+    unsigned int u = (unsigned int)h[i] << 16;
+    float f;
+    std::memcpy(&f, &u, 4);
+    f *= 0.0883883f * 1.44269504f;
+    std::memcpy(&u, &f, 4);
+    h[i] = (unsigned short)((u + 0x7fff + ((u >> 16) & 1)) >> 16);
+  }
+  hipMemcpy(qkv, h.data(), qn * 2, hipMemcpyHostToDevice);
+  for (int it = 0; it < 5; ++it) qie_attention_fwd_log2q_bf16(qkv, B, H, s_pad, kv, oi, ot, S_IMG, S_TXT, nullptr, 0, nullptr);
+  hipDeviceSynchronize();
+  hipMemcpyToSymbol(HIP_SYMBOL(g_stamp), z, sizeof(z));
+  hipEventRecord(a);
+  qie_attention_fwd_log2q_bf16(qkv, B, H, s_pad, kv, oi, ot, S_IMG, S_TXT, nullptr, 0, nullptr);
+  hipEventRecord(b);
+  hipDeviceSynchronize();
+  hipEventElapsedTime(&ms, a, b);
+  hipMemcpyFromSymbol(st, HIP_SYMBOL(g_stamp), sizeof(st));
+  printf("attention log2q %.3f ms (stamped build)\n", ms);
+  for (int g = 0; g < 2; ++g) {
+    const double nt = (double)st[g][3];
+    printf("group %d: tiles %.0f  M-body %.0f  M-end wait+barrier %.0f  V-phase %.0f  cycles/tile (s_memtime)\n",
+           g, nt, st[g][0] / nt, st[g][1] / nt, st[g][2] / nt);
+  }
   return 0;
 }
