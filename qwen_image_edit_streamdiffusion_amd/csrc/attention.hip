@@ -70,6 +70,9 @@ constexpr int kRing = 3;
 #ifndef QIE_ATTN_VPRIO  // ... and in its softmax phase
 #define QIE_ATTN_VPRIO 0
 #endif
+#ifndef QIE_ATTN_ONES  // 1: row sums by 4 MFMAs against a ones operand in the MFMA phase (log2q path)
+#define QIE_ATTN_ONES 0
+#endif
 #ifndef QIE_ATTN_ABL  // diagnostic ablations (wrong results): 1 no K/V DMA in the loop, 2 no exp2
 #define QIE_ATTN_ABL 0
 #endif
@@ -127,6 +130,7 @@ __device__ __forceinline__ void rfence(T& x) {
 struct PPState {
   f32x16_t s[2];
   f32x16_t negm;  // PRE: splat(-m_run), the C operand of each tile's first QK^T MFMA
+  f32x16_t lsum;  // PRE && QIE_ATTN_ONES: every element = the lane's query row sum
   f32x16_t o[4];
   bf16x8_t pf[4];
   bf16x8_t qf[8];
@@ -176,6 +180,9 @@ __global__ void __launch_bounds__(512) attn_pp_kernel(AttnArgs a) {
   const int ntiles = chunk < 0 ? ntot : (chunk + 1) * ntot / a.split;
 
   PPState st;
+  bf16x8_t ones;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) ones[k] = (__bf16)1.0f;
 #ifdef QIE_ATTN_STAMP
   unsigned long long acc_st[6] = {0, 0, 0, 0, 0, 0};
 #endif
@@ -260,6 +267,9 @@ __global__ void __launch_bounds__(512) attn_pp_kernel(AttnArgs a) {
     for (int i = i0; i < i1; ++i) {
       if (i + PF < i1) A[(i + PF) & 7] = opA(i + PF, tk, tv);
       mfma_i(i, A[i & 7]);
+      if constexpr (PRE && QIE_ATTN_ONES && i1 == 32) {  // row sums of P(t-1), beside the PV MFMAs
+        if (i >= 16 && ((i - 16) & 3) == 3) mma32(st.lsum, ones, st.pf[(i - 16) >> 2]);
+      }
     }
     __builtin_amdgcn_s_setprio(QIE_ATTN_VPRIO);
   };
@@ -306,8 +316,10 @@ __global__ void __launch_bounds__(512) attn_pp_kernel(AttnArgs a) {
         for (int r = 0; r < 16; r += 2) {
           const float p0 = __builtin_amdgcn_exp2f(st.s[cb][r]);
           const float p1 = __builtin_amdgcn_exp2f(st.s[cb][r + 1]);
-          ps0 += p0;
-          ps1 += p1;
+          if (!(PRE && QIE_ATTN_ONES)) {
+            ps0 += p0;
+            ps1 += p1;
+          }
           st.pf[cb * 2 + (r >> 3)][r & 7] = (__bf16)p0;
           st.pf[cb * 2 + (r >> 3)][(r & 7) + 1] = (__bf16)p1;
         }
@@ -320,6 +332,7 @@ __global__ void __launch_bounds__(512) attn_pp_kernel(AttnArgs a) {
         const float alpha = __builtin_amdgcn_exp2f(-d);
         st.m_run += d;
         st.l_run *= alpha;
+        if constexpr (QIE_ATTN_ONES) st.lsum *= alpha;
 #pragma unroll
         for (int db = 0; db < 4; ++db) st.o[db] *= alpha;
 #pragma unroll
@@ -362,6 +375,7 @@ __global__ void __launch_bounds__(512) attn_pp_kernel(AttnArgs a) {
     rfence(st.l_run);  // keep the row-sum adds in this phase (hipcc sinks them into the M-phase)
     rfence(st.m_run);
     if constexpr (PRE) rfence(st.negm);
+    if constexpr (PRE && QIE_ATTN_ONES) rfence(st.lsum);
 #pragma unroll
     for (int db = 0; db < 4; ++db) rfence(st.o[db]);
     if (pieces == 4) asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
@@ -395,6 +409,7 @@ __global__ void __launch_bounds__(512) attn_pp_kernel(AttnArgs a) {
   st.m_run = PRE ? 0.f : -INFINITY;  // PRE: finite (it is the MFMA's C); tile t0 sets it
   st.l_run = 0.f;
   if constexpr (PRE) st.negm = f32x16_t{};
+  if constexpr (PRE && QIE_ATTN_ONES) st.lsum = f32x16_t{};
 
   auto mend = [&](int) { asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory"); };
   mphase(I0{}, I16{}, t0, t0);  // S(t0)
@@ -421,7 +436,13 @@ __global__ void __launch_bounds__(512) attn_pp_kernel(AttnArgs a) {
   if (grp == 0) asm volatile("s_barrier" ::: "memory");
   // MFMA D -> VALU read hazard before the epilogue reads O (asm MFMAs are not padded by hipcc)
   asm volatile("s_nop 15\n\ts_nop 7" : "+v"(st.o[0]), "+v"(st.o[1]), "+v"(st.o[2]), "+v"(st.o[3]));
-  const float l_tot = st.l_run + __shfl_xor(st.l_run, 32, 64);
+  float l_tot;
+  if constexpr (PRE && QIE_ATTN_ONES) {
+    asm volatile("s_nop 7" : "+v"(st.lsum));
+    l_tot = st.lsum[0];  // the MFMA summed all 64 keys of every tile into each row of the column
+  } else {
+    l_tot = st.l_run + __shfl_xor(st.l_run, 32, 64);
+  }
   if (chunk >= 0) {  // fp32 partial: unnormalised O (d = 32db + 8g + 4hf + 0..3), row max, row sum
     float* po = a.ws + (((int64_t)bh * a.split + chunk) * kQB + q_loc) * kDh;
     float* pml = a.ws + (int64_t)a.B * a.H * a.split * kQB * kDh;
