@@ -303,9 +303,10 @@ int qie_vae_rms_norm_bf16(const void* x, const void* gamma, void* y, int64_t pix
                           qie_stream_t stream);
 
 /* Row softmax of fp32 scores: p = bf16(exp(scale * (s - max)) / sum) for columns < N, zero in
- * [N, ldp) (the K padding of the P.V GEMM). Row strides lds (floats), ldp (bf16); N % 4 == 0. */
+ * [N, ldp) (the K padding of the P.V GEMM). Row strides lds (floats), ldp (bf16); N % 4 == 0.
+ * causal != 0: row r keeps only columns 0..r (the prompt encoder's decoder mask). */
 int qie_softmax_rows_f32_bf16(const float* s, int64_t lds, void* p, int64_t ldp, int rows, int N, float scale,
-                              qie_stream_t stream);
+                              int causal, qie_stream_t stream);
 
 /* y[c][r] = x[r][c] for an R x C bf16 block (row strides ldx, ldy elements). */
 int qie_transpose_bf16(const void* x, int64_t ldx, void* y, int64_t ldy, int R, int C, qie_stream_t stream);
@@ -323,6 +324,24 @@ int qie_vae_latents_out_bf16(const void* x, int64_t ldx, int batch, int h, int w
 /* Decoder output [pixels][ldx] bf16 (channels 0..2) -> clamp(-1, 1) -> (x/2 + 0.5).clamp(0, 1)
  * -> round(255 v) as uint8 RGB [pixels][3] (VaeImageProcessor.postprocess, output_type="pil"). */
 int qie_vae_rgb_out(const void* x, int64_t ldx, void* rgb, int64_t pixels, qie_stream_t stream);
+
+/* ------------------------------------------------------------------ prompt encoder (§8 f2)
+ * The Qwen2.5-VL language model of the prompt encoder (text_encoder, transformers
+ * Qwen2_5_VLTextModel [U]); its projections / norms / attention products use the entry points
+ * above (qie_linear*, qie_rmsnorm_bf16, qie_matmul_f32out_bf16, qie_softmax_rows_f32_bf16). */
+
+/* out[i] = table[ids[i]] (embed_tokens), D % 8 == 0; ids are device int32, clamped to the vocab. */
+int qie_embed_rows_bf16(const void* table, const int* ids_dev, int rows, int D, int vocab, void* out,
+                        qie_stream_t stream);
+
+/* apply_multimodal_rotary_pos_emb on heads [h0, h0 + nh) of each row, in place: rotate_half form,
+ * x = bf16(bf16(x cos) + bf16(rotate_half(x) sin)) with per-row bf16 tables [rows][head_dim]
+ * (the temporal / height / width sections already merged on the host). */
+int qie_rope_half_bf16(void* x, int64_t ld, int rows, int h0, int nh, int head_dim, const void* cos_tab,
+                       const void* sin_tab, qie_stream_t stream);
+
+/* Qwen2MLP gating: y = bf16(bf16(silu(g)) * u) with [g | u] = gu[r][0..F) | gu[r][F..2F). */
+int qie_silu_mul_bf16(const void* gu, int64_t ldg, int rows, int F, void* y, int64_t ldy, qie_stream_t stream);
 
 #ifdef __cplusplus
 }

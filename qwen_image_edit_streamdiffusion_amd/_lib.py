@@ -68,11 +68,14 @@ SIGNATURES = {
     "qie_matmul_f32out_bf16": [P, L, P, L, P, I, I, I, P],
     "qie_vae_latents_in_bf16": [P, I, I, I, P, P, P, P, P, P],
     "qie_vae_rms_norm_bf16": [P, P, P, L, I, I, P],
-    "qie_softmax_rows_f32_bf16": [P, L, P, L, I, I, F, P],
+    "qie_softmax_rows_f32_bf16": [P, L, P, L, I, I, F, I, P],
     "qie_transpose_bf16": [P, L, P, L, I, I, P],
     "qie_vae_rgb_out": [P, L, P, L, P],
     "qie_vae_rgb_in": [P, P, L, P],
     "qie_vae_latents_out_bf16": [P, L, I, I, I, P, P, P, P],
+    "qie_embed_rows_bf16": [P, P, I, I, I, P, P],
+    "qie_rope_half_bf16": [P, L, I, I, I, I, P, P, P],
+    "qie_silu_mul_bf16": [P, L, I, I, P, L, P],
 }
 _RESTYPES = {"qie_strerror": c_char_p}
 

@@ -104,15 +104,20 @@ __device__ __forceinline__ void ml_merge(float& m, float& l, float m2, float l2)
 }
 
 __global__ void __launch_bounds__(256)
-    softmax_rows_kernel(const float* __restrict__ s, int64_t lds, bf16_t* __restrict__ p, int64_t ldp, int N,
-                        float scale) {
+    softmax_rows_kernel(const float* __restrict__ s, int64_t lds, bf16_t* __restrict__ p, int64_t ldp, int Nall,
+                        float scale, int causal) {
   const int64_t row = blockIdx.x;
+  // causal (the text encoder's decoder mask): row r sees keys 0..r; others see all Nall
+  const int N = causal ? min(Nall, (int)row + 1) : Nall;
   const float* sr = s + row * lds;
   __shared__ float red_m[4], red_l[4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   float m = -INFINITY, l = 0.f;  // in scaled units
   for (int c = tid * 4; c < N; c += 1024) {
-    const f32x4_t t = *(const f32x4_t*)(sr + c);
+    f32x4_t t = *(const f32x4_t*)(sr + c);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (c + k >= N) t[k] = -INFINITY;  // causal: the chunk straddling the diagonal
     const float tm = fmaxf(fmaxf(t[0], t[1]), fmaxf(t[2], t[3])) * scale;
     float tl = 0.f;
 #pragma unroll
@@ -132,11 +137,13 @@ __global__ void __launch_bounds__(256)
   const float inv = 1.0f / l;
   bf16_t* pr = p + row * ldp;
   for (int c = tid * 4; c < N; c += 1024) {
-    const f32x4_t t = *(const f32x4_t*)(sr + c);
-    *(u32x2_t*)(pr + c) = u32x2_t{pack2(__expf(t[0] * scale - m) * inv, __expf(t[1] * scale - m) * inv),
-                                  pack2(__expf(t[2] * scale - m) * inv, __expf(t[3] * scale - m) * inv)};
+    f32x4_t t = *(const f32x4_t*)(sr + c);
+    float e[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) e[k] = c + k < N ? __expf(t[k] * scale - m) * inv : 0.f;
+    *(u32x2_t*)(pr + c) = u32x2_t{pack2(e[0], e[1]), pack2(e[2], e[3])};
   }
-  for (int c = N + tid * 4; c < ldp; c += 1024) *(u32x2_t*)(pr + c) = u32x2_t{0u, 0u};
+  for (int c = ((N + 3) & ~3) + tid * 4; c < ldp; c += 1024) *(u32x2_t*)(pr + c) = u32x2_t{0u, 0u};
 }
 
 // ---- bf16 transpose: y[c][r] = x[r][c] for a [R][C] block with row stride ldx; 64x64 LDS tiles
@@ -237,10 +244,10 @@ extern "C" int qie_vae_rms_norm_bf16(const void* x, const void* gamma, void* y, 
 }
 
 extern "C" int qie_softmax_rows_f32_bf16(const float* s, int64_t lds, void* p, int64_t ldp, int rows, int N,
-                                         float scale, qie_stream_t stream) {
+                                         float scale, int causal, qie_stream_t stream) {
   QIE_CHECK_ARG(s && p && rows > 0 && N > 0 && N % 4 == 0 && lds >= N && lds % 4 == 0);
   QIE_CHECK_ARG(ldp >= N && ldp % 4 == 0 && ((uintptr_t)s % 16) == 0 && ((uintptr_t)p % 8) == 0);
-  softmax_rows_kernel<<<rows, 256, 0, (hipStream_t)stream>>>(s, lds, (bf16_t*)p, ldp, N, scale);
+  softmax_rows_kernel<<<rows, 256, 0, (hipStream_t)stream>>>(s, lds, (bf16_t*)p, ldp, N, scale, causal);
   return qie_last_error();
 }
 

@@ -474,16 +474,19 @@ def matmul_f32out(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] 
     return out
 
 
-def softmax_rows(s: torch.Tensor, scale: float, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+def softmax_rows(s: torch.Tensor, scale: float, out: Optional[torch.Tensor] = None,
+                 causal: bool = False) -> torch.Tensor:
     """bf16 softmax(scale * s) per row of fp32 s [R, N]; ``out`` [R, >=N] (a row-major view whose
-    columns past N -- the K padding of a following GEMM -- are zero-filled)."""
+    columns past N -- the K padding of a following GEMM -- are zero-filled). ``causal``: row r
+    keeps columns 0..r."""
     _dev(s, out)
     _chk(s.dtype == torch.float32 and _is2d_rowmajor(s), "fp32 [rows, N]")
     R, N = s.shape
     if out is None:
         out = torch.empty(R, N, dtype=BF16, device=s.device)
     _chk(_is2d_rowmajor(out) and out.shape[0] == R and out.shape[1] >= N and out.dtype == BF16, "out")
-    _lib.call("qie_softmax_rows_f32_bf16", _p(s), s.stride(0), _p(out), out.shape[1], R, N, scale, _stream())
+    _lib.call("qie_softmax_rows_f32_bf16", _p(s), s.stride(0), _p(out), out.shape[1], R, N, scale, int(causal),
+              _stream())
     return out
 
 
@@ -555,4 +558,36 @@ def vae_latents_out(x: torch.Tensor, B: int, h: int, w: int, mean: torch.Tensor,
         out = torch.empty(B, h * w // 4, 64, dtype=BF16, device=x.device)
     _chk(out.shape == (B, h * w // 4, 64) and out.is_contiguous(), "out")
     _lib.call("qie_vae_latents_out_bf16", _p(x), x.stride(0), B, h, w, _p(mean), _p(std), _p(out), _stream())
+    return out
+
+
+# ---------------------------------------------------------------------------- prompt encoder (§8 f2)
+def embed_rows(table: torch.Tensor, ids: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    _dev(table, ids, out)
+    _chk(table.dtype == BF16 and table.is_contiguous() and ids.dtype == torch.int32 and ids.is_contiguous(), "embed")
+    V, D = table.shape
+    if out is None:
+        out = torch.empty(ids.numel(), D, dtype=BF16, device=table.device)
+    _chk(out.shape == (ids.numel(), D) and out.is_contiguous(), "out")
+    _lib.call("qie_embed_rows_bf16", _p(table), _p(ids), ids.numel(), D, V, _p(out), _stream())
+    return out
+
+
+def rope_half(x: torch.Tensor, h0: int, nh: int, head_dim: int, cos: torch.Tensor, sin: torch.Tensor):
+    """In-place rotate-half RoPE on heads [h0, h0 + nh) of the rows of x (row-major view)."""
+    _dev(x, cos, sin)
+    _chk(x.dtype == BF16 and _is2d_rowmajor(x) and cos.dtype == BF16 and sin.dtype == BF16, "rope dtypes")
+    _chk(cos.shape == sin.shape == (x.shape[0], head_dim) and cos.is_contiguous() and sin.is_contiguous(), "tables")
+    _lib.call("qie_rope_half_bf16", _p(x), x.stride(0), x.shape[0], h0, nh, head_dim, _p(cos), _p(sin), _stream())
+
+
+def silu_mul(gu: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """[g | u] rows -> bf16(bf16(silu(g)) * u)."""
+    _dev(gu, out)
+    _chk(gu.dtype == BF16 and _is2d_rowmajor(gu) and gu.shape[1] % 2 == 0, "gu [R, 2F]")
+    R, F = gu.shape[0], gu.shape[1] // 2
+    if out is None:
+        out = torch.empty(R, F, dtype=BF16, device=gu.device)
+    _chk(_is2d_rowmajor(out) and out.shape == (R, F), "out [R, F]")
+    _lib.call("qie_silu_mul_bf16", _p(gu), gu.stride(0), R, F, _p(out), out.stride(0), _stream())
     return out
