@@ -308,6 +308,13 @@ int qie_vae_rms_norm_bf16(const void* x, const void* gamma, void* y, int64_t pix
 int qie_softmax_rows_f32_bf16(const float* s, int64_t lds, void* p, int64_t ldp, int rows, int N, float scale,
                               int causal, qie_stream_t stream);
 
+/* As qie_softmax_rows_f32_bf16 with row r restricted to keys [ranges[2r], ranges[2r+1]) (device
+ * int32 pairs): the vision tower's block-diagonal masks -- windows of cu_window_seqlens and
+ * per-image full attention of cu_seqlens (transformers Qwen2_5_VLVisionAttention's per-chunk
+ * split). Columns outside the range are written 0 up to ldp. */
+int qie_softmax_rows_ranged_f32_bf16(const float* s, int64_t lds, void* p, int64_t ldp, int rows, int N,
+                                     float scale, const int* ranges_dev, qie_stream_t stream);
+
 /* y[c][r] = x[r][c] for an R x C bf16 block (row strides ldx, ldy elements). */
 int qie_transpose_bf16(const void* x, int64_t ldx, void* y, int64_t ldy, int R, int C, qie_stream_t stream);
 
@@ -334,11 +341,17 @@ int qie_vae_rgb_out(const void* x, int64_t ldx, void* rgb, int64_t pixels, qie_s
 int qie_embed_rows_bf16(const void* table, const int* ids_dev, int rows, int D, int vocab, void* out,
                         qie_stream_t stream);
 
-/* apply_multimodal_rotary_pos_emb on heads [h0, h0 + nh) of each row, in place: rotate_half form,
- * x = bf16(bf16(x cos) + bf16(rotate_half(x) sin)) with per-row bf16 tables [rows][head_dim]
- * (the temporal / height / width sections already merged on the host). */
-int qie_rope_half_bf16(void* x, int64_t ld, int rows, int h0, int nh, int head_dim, const void* cos_tab,
-                       const void* sin_tab, qie_stream_t stream);
+/* Rotate-half RoPE in place on heads [h0, h0 + nh) of each row (rotary width head_dim, heads
+ * head_stride elements apart -- the vision tower pads its 80-wide heads to 128 slots), per-row
+ * tables [rows][head_dim] with the sections already merged on the host:
+ *   tab_f32 = 0: bf16 tables, apply_multimodal_rotary_pos_emb in the activation dtype,
+ *                x = bf16(bf16(x cos) + bf16(rotate_half(x) sin));
+ *   tab_f32 = 1: fp32 tables, apply_rotary_pos_emb_vision (upcast), x = bf16(x cos + rot(x) sin). */
+int qie_rope_half_bf16(void* x, int64_t ld, int rows, int h0, int nh, int head_dim, int head_stride,
+                       const void* cos_tab, const void* sin_tab, int tab_f32, qie_stream_t stream);
+
+/* nn.GELU() (erf form) in place on a bf16 [rows][n] block (row stride ld): the patch merger. */
+int qie_gelu_erf_bf16(void* x, int64_t ld, int rows, int n, qie_stream_t stream);
 
 /* Qwen2MLP gating: y = bf16(bf16(silu(g)) * u) with [g | u] = gu[r][0..F) | gu[r][F..2F). */
 int qie_silu_mul_bf16(const void* gu, int64_t ldg, int rows, int F, void* y, int64_t ldy, qie_stream_t stream);

@@ -69,3 +69,53 @@ def rotary_reference(hidden: int, heads: int, mrope, position_ids: torch.Tensor,
     cos, sin = rot(x, position_ids.view(3, 1, -1))
     qe, _ = apply_multimodal_rotary_pos_emb(x, x, cos, sin, list(mrope))
     return qe[0].permute(1, 0, 2)
+
+
+def tiny_vl_model(seed: int = 0, text_hidden: int = 256, vis_hidden: int = 320, vis_heads: int = 4,
+                  vis_intermediate: int = 200, depth: int = 4, fullatt=(1, 3), image_token_id: int = 990):
+    """A random transformers Qwen2_5_VLModel (vision tower + language model, fp32 eager) whose
+    weights are bf16-representable, and its state_dict. The vision head_dim is 80 (as in the 7B
+    checkpoint) and the MLP width 200 is not a multiple of 64 (the HIP path pads both)."""
+    from transformers import Qwen2_5_VLConfig
+    from transformers.models.qwen2_5_vl.modeling_qwen2_5_vl import Qwen2_5_VLModel
+    cfg = Qwen2_5_VLConfig(
+        text_config=dict(vocab_size=1000, hidden_size=text_hidden, bos_token_id=0, eos_token_id=1, intermediate_size=512, num_hidden_layers=2,
+                         num_attention_heads=2, num_key_value_heads=1, rms_norm_eps=1e-6,
+                         rope_parameters={"rope_type": "default", "rope_theta": 1e6, "mrope_section": [16, 24, 24]}),
+        vision_config=dict(depth=depth, hidden_size=vis_hidden, intermediate_size=vis_intermediate,
+                           num_heads=vis_heads, out_hidden_size=text_hidden, fullatt_block_indexes=list(fullatt),
+                           window_size=112, patch_size=14, spatial_merge_size=2, temporal_patch_size=2),
+        bos_token_id=0, eos_token_id=1, image_token_id=image_token_id, video_token_id=991, vision_start_token_id=992, vision_end_token_id=993)
+    cfg._attn_implementation = "eager"
+    cfg.text_config._attn_implementation = "eager"
+    cfg.vision_config._attn_implementation = "eager"
+    torch.manual_seed(seed)
+    m = Qwen2_5_VLModel(cfg).eval()
+    with torch.no_grad():
+        for name, p in m.named_parameters():
+            if "norm" in name or "ln_q" in name:
+                p.copy_(1.0 + 0.1 * torch.randn_like(p))
+            elif name.endswith("bias"):
+                p.copy_(0.1 * torch.randn_like(p))
+            else:
+                p.copy_(torch.randn_like(p) / (p[0].numel() ** 0.5))
+            p.copy_(p.to(BF16).float())
+    return m, {k: v.to(BF16) for k, v in m.state_dict().items()}
+
+
+@torch.no_grad()
+def vision_forward(m, pixel_values: torch.Tensor, grid_thw: torch.Tensor) -> torch.Tensor:
+    """The tower's pooler output (merged embeddings, raster order), fp32."""
+    return m.visual(pixel_values.float(), grid_thw=grid_thw).pooler_output
+
+
+@torch.no_grad()
+def vl_forward(m, input_ids: torch.Tensor, pixel_values=None, image_grid_thw=None) -> torch.Tensor:
+    """Qwen2_5_VLModel last hidden state for one prompt (the reference's hidden_states[-1])."""
+    ids = input_ids.view(1, -1)
+    kw = {}
+    if pixel_values is not None:
+        kw = dict(pixel_values=pixel_values.float(), image_grid_thw=image_grid_thw,
+                  mm_token_type_ids=(ids == m.config.image_token_id).int())
+    out = m(input_ids=ids, output_hidden_states=True, **kw)
+    return out.hidden_states[-1][0], out.last_hidden_state[0]

@@ -105,19 +105,25 @@ __device__ __forceinline__ void ml_merge(float& m, float& l, float m2, float l2)
 
 __global__ void __launch_bounds__(256)
     softmax_rows_kernel(const float* __restrict__ s, int64_t lds, bf16_t* __restrict__ p, int64_t ldp, int Nall,
-                        float scale, int causal) {
+                        float scale, int causal, const int* __restrict__ ranges) {
   const int64_t row = blockIdx.x;
-  // causal (the text encoder's decoder mask): row r sees keys 0..r; others see all Nall
-  const int N = causal ? min(Nall, (int)row + 1) : Nall;
+  // Keys [c0, c1) of row r: all Nall; causal (the text encoder's decoder mask) 0..r; ranges (the
+  // vision tower's window / per-image blocks) ranges[2r] .. ranges[2r+1]. Other columns are 0.
+  int c0 = 0, c1 = Nall;
+  if (causal) c1 = min(Nall, (int)row + 1);
+  if (ranges) {
+    c0 = max(ranges[2 * row], 0);
+    c1 = min(ranges[2 * row + 1], Nall);
+  }
   const float* sr = s + row * lds;
   __shared__ float red_m[4], red_l[4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   float m = -INFINITY, l = 0.f;  // in scaled units
-  for (int c = tid * 4; c < N; c += 1024) {
+  for (int c = (c0 & ~3) + tid * 4; c < c1; c += 1024) {
     f32x4_t t = *(const f32x4_t*)(sr + c);
 #pragma unroll
     for (int k = 0; k < 4; ++k)
-      if (c + k >= N) t[k] = -INFINITY;  // causal: the chunk straddling the diagonal
+      if (c + k < c0 || c + k >= c1) t[k] = -INFINITY;  // the chunks straddling the range ends
     const float tm = fmaxf(fmaxf(t[0], t[1]), fmaxf(t[2], t[3])) * scale;
     float tl = 0.f;
 #pragma unroll
@@ -136,14 +142,16 @@ __global__ void __launch_bounds__(256)
   for (int w = 1; w < 4; ++w) ml_merge(m, l, red_m[w], red_l[w]);
   const float inv = 1.0f / l;
   bf16_t* pr = p + row * ldp;
-  for (int c = tid * 4; c < N; c += 1024) {
-    f32x4_t t = *(const f32x4_t*)(sr + c);
-    float e[4];
+  for (int c = tid * 4; c < ldp; c += 1024) {
+    float e[4] = {0.f, 0.f, 0.f, 0.f};
+    if (c + 3 >= c0 && c < c1) {
+      const f32x4_t t = *(const f32x4_t*)(sr + c);
 #pragma unroll
-    for (int k = 0; k < 4; ++k) e[k] = c + k < N ? __expf(t[k] * scale - m) * inv : 0.f;
+      for (int k = 0; k < 4; ++k)
+        if (c + k >= c0 && c + k < c1) e[k] = __expf(t[k] * scale - m) * inv;
+    }
     *(u32x2_t*)(pr + c) = u32x2_t{pack2(e[0], e[1]), pack2(e[2], e[3])};
   }
-  for (int c = ((N + 3) & ~3) + tid * 4; c < ldp; c += 1024) *(u32x2_t*)(pr + c) = u32x2_t{0u, 0u};
 }
 
 // ---- bf16 transpose: y[c][r] = x[r][c] for a [R][C] block with row stride ldx; 64x64 LDS tiles
@@ -247,7 +255,15 @@ extern "C" int qie_softmax_rows_f32_bf16(const float* s, int64_t lds, void* p, i
                                          float scale, int causal, qie_stream_t stream) {
   QIE_CHECK_ARG(s && p && rows > 0 && N > 0 && N % 4 == 0 && lds >= N && lds % 4 == 0);
   QIE_CHECK_ARG(ldp >= N && ldp % 4 == 0 && ((uintptr_t)s % 16) == 0 && ((uintptr_t)p % 8) == 0);
-  softmax_rows_kernel<<<rows, 256, 0, (hipStream_t)stream>>>(s, lds, (bf16_t*)p, ldp, N, scale, causal);
+  softmax_rows_kernel<<<rows, 256, 0, (hipStream_t)stream>>>(s, lds, (bf16_t*)p, ldp, N, scale, causal, nullptr);
+  return qie_last_error();
+}
+
+extern "C" int qie_softmax_rows_ranged_f32_bf16(const float* s, int64_t lds, void* p, int64_t ldp, int rows, int N,
+                                                float scale, const int* ranges_dev, qie_stream_t stream) {
+  QIE_CHECK_ARG(s && p && ranges_dev && rows > 0 && N > 0 && N % 4 == 0 && lds >= N && lds % 4 == 0);
+  QIE_CHECK_ARG(ldp >= N && ldp % 4 == 0 && ((uintptr_t)s % 16) == 0 && ((uintptr_t)p % 8) == 0);
+  softmax_rows_kernel<<<rows, 256, 0, (hipStream_t)stream>>>(s, lds, (bf16_t*)p, ldp, N, scale, 0, ranges_dev);
   return qie_last_error();
 }
 

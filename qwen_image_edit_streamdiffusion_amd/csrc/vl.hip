@@ -1,5 +1,5 @@
-// Qwen2.5-VL language model pieces (the prompt encoder): token embedding
-// gather, multimodal rotate-half RoPE, SwiGLU gating. The projections, RMSNorms and the
+// Qwen2.5-VL prompt-encoder pieces: row gather (token embedding, window
+// permutation), rotate-half RoPE (3-D M-RoPE tables / 2-D vision tables), SwiGLU gating, erf GELU. The projections, RMSNorms and the
 // attention products run on the GEMM / norm kernels of gemm.hip / norm.hip / vae.hip.
 //
 // Rounding points follow transformers' Qwen2_5_VLTextModel in bf16 [U: transformers 5.15
@@ -22,27 +22,58 @@ __global__ void __launch_bounds__(256)
   *(u32x4_t*)(out + (int64_t)r * D + c * 8) = *(const u32x4_t*)(table + (int64_t)id * D + c * 8);
 }
 
-// In place on heads [h0, h0 + nh) of each row (head_dim Dh, row stride ld): for d < Dh/2,
-//   x[d]        <- bf16(bf16(x[d] cos[d])        + bf16(-x[d + Dh/2] sin[d]))
-//   x[d + Dh/2] <- bf16(bf16(x[d + Dh/2] cos[d + Dh/2]) + bf16(x[d] sin[d + Dh/2]))
-// with the per-row bf16 tables cos / sin [rows][Dh] (the M-RoPE sections already merged).
+// In place on heads [h0, h0 + nh) of each row (rotary width Dh, heads hs elements apart, row
+// stride ld), with per-row tables cos / sin [rows][Dh] (the M-RoPE sections already merged):
+//   bf16 tables (the language model): three bf16 roundings, as in the activation dtype
+//     x[d]        <- bf16(bf16(x[d] cos[d])        + bf16(-x[d + Dh/2] sin[d]))
+//     x[d + Dh/2] <- bf16(bf16(x[d + Dh/2] cos[d + Dh/2]) + bf16(x[d] sin[d + Dh/2]))
+//   fp32 tables (the vision tower, apply_rotary_pos_emb_vision upcasts): fp32 products and sum,
+//   one bf16 rounding (unfused, as torch evaluates q * cos + rotate_half(q) * sin).
+template <bool F32TAB>
 __global__ void __launch_bounds__(256)
-    rope_half_kernel(bf16_t* __restrict__ x, int64_t ld, int rows, int h0, int nh, int Dh,
-                     const bf16_t* __restrict__ cs, const bf16_t* __restrict__ sn) {
+    rope_half_kernel(bf16_t* __restrict__ x, int64_t ld, int rows, int h0, int nh, int Dh, int hs,
+                     const void* __restrict__ cs_, const void* __restrict__ sn_) {
   const int half = Dh >> 1;
   const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (q >= (int64_t)rows * nh * half) return;
   const int d = (int)(q % half);
   const int64_t rh = q / half;
   const int h = (int)(rh % nh), r = (int)(rh / nh);
-  bf16_t* p = x + (int64_t)r * ld + (int64_t)(h0 + h) * Dh;
+  bf16_t* p = x + (int64_t)r * ld + (int64_t)(h0 + h) * hs;
   const float a = bf2f(p[d]), b = bf2f(p[d + half]);
-  const bf16_t* cr = cs + (int64_t)r * Dh;
-  const bf16_t* sr = sn + (int64_t)r * Dh;
-  const float lo = rbf(rbf(a * bf2f(cr[d])) + rbf(-b * bf2f(sr[d])));
-  const float hi = rbf(rbf(b * bf2f(cr[d + half])) + rbf(a * bf2f(sr[d + half])));
+  float lo, hi;
+  if constexpr (F32TAB) {
+    const float* cr = (const float*)cs_ + (int64_t)r * Dh;
+    const float* sr = (const float*)sn_ + (int64_t)r * Dh;
+    lo = __fadd_rn(__fmul_rn(a, cr[d]), __fmul_rn(-b, sr[d]));
+    hi = __fadd_rn(__fmul_rn(b, cr[d + half]), __fmul_rn(a, sr[d + half]));
+  } else {
+    const bf16_t* cr = (const bf16_t*)cs_ + (int64_t)r * Dh;
+    const bf16_t* sr = (const bf16_t*)sn_ + (int64_t)r * Dh;
+    lo = rbf(rbf(a * bf2f(cr[d])) + rbf(-b * bf2f(sr[d])));
+    hi = rbf(rbf(b * bf2f(cr[d + half])) + rbf(a * bf2f(sr[d + half])));
+  }
   p[d] = f2bf(lo);
   p[d + half] = f2bf(hi);
+}
+
+// y = bf16(gelu_erf(x)) elementwise over [rows][n] (nn.GELU() default, on a bf16 tensor)
+__global__ void __launch_bounds__(256)
+    gelu_erf_kernel(bf16_t* __restrict__ x, int64_t ld, int rows, int n) {
+  const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int nch = n >> 3;
+  if (q >= (int64_t)rows * nch) return;
+  const int r = (int)(q / nch), c = (int)(q - (int64_t)r * nch);
+  bf16_t* p = x + (int64_t)r * ld + c * 8;
+  const u32x4_t w = *(const u32x4_t*)p;
+  const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
+  uint32_t o[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float a = lo_f(ww[k]), b = hi_f(ww[k]);
+    o[k] = pack2(0.5f * a * (1.0f + erff(a * 0.70710678118654752f)), 0.5f * b * (1.0f + erff(b * 0.70710678118654752f)));
+  }
+  *(u32x4_t*)p = u32x4_t{o[0], o[1], o[2], o[3]};
 }
 
 // y[r][f] = bf16(bf16(silu(g)) * u), g = gu[r][f], u = gu[r][F + f] (packed gate | up GEMM output)
@@ -78,13 +109,25 @@ extern "C" int qie_embed_rows_bf16(const void* table, const int* ids_dev, int ro
   return qie_last_error();
 }
 
-extern "C" int qie_rope_half_bf16(void* x, int64_t ld, int rows, int h0, int nh, int head_dim, const void* cos_tab,
-                                  const void* sin_tab, qie_stream_t stream) {
+extern "C" int qie_rope_half_bf16(void* x, int64_t ld, int rows, int h0, int nh, int head_dim, int head_stride,
+                                  const void* cos_tab, const void* sin_tab, int tab_f32, qie_stream_t stream) {
   QIE_CHECK_ARG(x && cos_tab && sin_tab && rows > 0 && h0 >= 0 && nh > 0 && head_dim > 0 && head_dim % 2 == 0);
-  QIE_CHECK_ARG(ld >= (int64_t)(h0 + nh) * head_dim);
+  QIE_CHECK_ARG(head_stride >= head_dim && ld >= (int64_t)(h0 + nh - 1) * head_stride + head_dim);
   const int64_t n = (int64_t)rows * nh * (head_dim / 2);
-  rope_half_kernel<<<(unsigned)((n + 255) / 256), 256, 0, (hipStream_t)stream>>>(
-      (bf16_t*)x, ld, rows, h0, nh, head_dim, (const bf16_t*)cos_tab, (const bf16_t*)sin_tab);
+  const unsigned g = (unsigned)((n + 255) / 256);
+  if (tab_f32)
+    rope_half_kernel<true><<<g, 256, 0, (hipStream_t)stream>>>((bf16_t*)x, ld, rows, h0, nh, head_dim, head_stride,
+                                                               cos_tab, sin_tab);
+  else
+    rope_half_kernel<false><<<g, 256, 0, (hipStream_t)stream>>>((bf16_t*)x, ld, rows, h0, nh, head_dim, head_stride,
+                                                                cos_tab, sin_tab);
+  return qie_last_error();
+}
+
+extern "C" int qie_gelu_erf_bf16(void* x, int64_t ld, int rows, int n, qie_stream_t stream) {
+  QIE_CHECK_ARG(x && rows > 0 && n > 0 && n % 8 == 0 && ld >= n && ld % 8 == 0 && ((uintptr_t)x % 16) == 0);
+  const int64_t t = (int64_t)rows * (n / 8);
+  gelu_erf_kernel<<<(unsigned)((t + 255) / 256), 256, 0, (hipStream_t)stream>>>((bf16_t*)x, ld, rows, n);
   return qie_last_error();
 }
 

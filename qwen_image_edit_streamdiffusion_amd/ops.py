@@ -475,18 +475,24 @@ def matmul_f32out(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] 
 
 
 def softmax_rows(s: torch.Tensor, scale: float, out: Optional[torch.Tensor] = None,
-                 causal: bool = False) -> torch.Tensor:
-    """bf16 softmax(scale * s) per row of fp32 s [R, N]; ``out`` [R, >=N] (a row-major view whose
-    columns past N -- the K padding of a following GEMM -- are zero-filled). ``causal``: row r
-    keeps columns 0..r."""
-    _dev(s, out)
+                 causal: bool = False, ranges: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """bf16 softmax(scale * s) per row of fp32 s [R, N]; ``out`` [R, >=N] (contiguous; columns past
+    N -- the K padding of a following GEMM -- are zero-filled). ``causal``: row r keeps columns
+    0..r; ``ranges`` (device int32 [R, 2]): row r keeps columns [ranges[r, 0], ranges[r, 1])."""
+    _dev(s, out, ranges)
     _chk(s.dtype == torch.float32 and _is2d_rowmajor(s), "fp32 [rows, N]")
     R, N = s.shape
     if out is None:
         out = torch.empty(R, N, dtype=BF16, device=s.device)
-    _chk(_is2d_rowmajor(out) and out.shape[0] == R and out.shape[1] >= N and out.dtype == BF16, "out")
-    _lib.call("qie_softmax_rows_f32_bf16", _p(s), s.stride(0), _p(out), out.shape[1], R, N, scale, int(causal),
-              _stream())
+    _chk(out.is_contiguous() and out.shape[0] == R and out.shape[1] >= N and out.dtype == BF16, "out")
+    if ranges is not None:
+        _chk(not causal and ranges.dtype == torch.int32 and ranges.is_contiguous() and ranges.shape == (R, 2),
+             "ranges int32 [rows, 2]")
+        _lib.call("qie_softmax_rows_ranged_f32_bf16", _p(s), s.stride(0), _p(out), out.shape[1], R, N, scale,
+                  _p(ranges), _stream())
+    else:
+        _lib.call("qie_softmax_rows_f32_bf16", _p(s), s.stride(0), _p(out), out.shape[1], R, N, scale,
+                  int(causal), _stream())
     return out
 
 
@@ -573,12 +579,28 @@ def embed_rows(table: torch.Tensor, ids: torch.Tensor, out: Optional[torch.Tenso
     return out
 
 
-def rope_half(x: torch.Tensor, h0: int, nh: int, head_dim: int, cos: torch.Tensor, sin: torch.Tensor):
-    """In-place rotate-half RoPE on heads [h0, h0 + nh) of the rows of x (row-major view)."""
+def rope_half(x: torch.Tensor, h0: int, nh: int, head_dim: int, cos: torch.Tensor, sin: torch.Tensor,
+              head_stride: Optional[int] = None):
+    """In-place rotate-half RoPE on heads [h0, h0 + nh) of the rows of x (row-major view), heads
+    ``head_stride`` (default head_dim) elements apart. bf16 tables: the language model's rounding;
+    fp32 tables: the vision tower's (one rounding)."""
     _dev(x, cos, sin)
-    _chk(x.dtype == BF16 and _is2d_rowmajor(x) and cos.dtype == BF16 and sin.dtype == BF16, "rope dtypes")
+    hs = head_dim if head_stride is None else head_stride
+    f32 = cos.dtype == torch.float32
+    _chk(x.dtype == BF16 and _is2d_rowmajor(x) and cos.dtype == sin.dtype and cos.dtype in (BF16, torch.float32),
+         "rope dtypes")
     _chk(cos.shape == sin.shape == (x.shape[0], head_dim) and cos.is_contiguous() and sin.is_contiguous(), "tables")
-    _lib.call("qie_rope_half_bf16", _p(x), x.stride(0), x.shape[0], h0, nh, head_dim, _p(cos), _p(sin), _stream())
+    _chk(hs >= head_dim and (h0 + nh - 1) * hs + head_dim <= x.shape[1], "heads exceed the row")
+    _lib.call("qie_rope_half_bf16", _p(x), x.stride(0), x.shape[0], h0, nh, head_dim, hs, _p(cos), _p(sin),
+              int(f32), _stream())
+
+
+def gelu_erf_(x: torch.Tensor) -> torch.Tensor:
+    """In-place nn.GELU() (erf form) on a bf16 row-major block."""
+    _dev(x)
+    _chk(x.dtype == BF16 and _is2d_rowmajor(x) and x.shape[1] % 8 == 0, "bf16 [rows, n % 8]")
+    _lib.call("qie_gelu_erf_bf16", _p(x), x.stride(0), x.shape[0], x.shape[1], _stream())
+    return x
 
 
 def silu_mul(gu: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:

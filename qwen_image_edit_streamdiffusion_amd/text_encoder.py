@@ -168,3 +168,154 @@ class QwenVLTextModel:
         return h[:S]
 
     __call__ = forward
+
+
+# ---------------------------------------------------------------------------- text + vision
+def rope_index(input_ids: torch.Tensor, image_token_id: int, image_grid_thw=None, spatial_merge_size: int = 2
+               ) -> torch.Tensor:
+    """3-D positions [3, S] for one prompt (Qwen2_5_VLModel.get_rope_index, images only): text runs
+    count up on all three axes; an image block of (t, h/m, w/m) merged tokens starting at position
+    p gets (p, p + row, p + col) (temporal interval 1 for images), and the text after it resumes at
+    p + max(h, w) / m."""
+    ids = input_ids.reshape(-1).cpu()
+    S = ids.numel()
+    grids = [tuple(int(v) for v in g) for g in (image_grid_thw.tolist() if torch.is_tensor(image_grid_thw)
+                                                 else (image_grid_thw or []))]
+    pos = torch.empty(3, S, dtype=torch.long)
+    is_img = (ids == image_token_id).tolist()
+    i, cur, gi = 0, 0, 0
+    while i < S:
+        j = i
+        while j < S and is_img[j] == is_img[i]:
+            j += 1
+        if not is_img[i]:
+            pos[:, i:j] = torch.arange(cur, cur + j - i)
+            cur += j - i
+        else:
+            if gi >= len(grids):
+                raise ValueError("more <|image_pad|> runs than image_grid_thw entries")
+            t, h, w = grids[gi]
+            gi += 1
+            lh, lw = h // spatial_merge_size, w // spatial_merge_size
+            n = t * lh * lw
+            if j - i != n:
+                raise ValueError(f"image token run of {j - i} != {n} merged patches")
+            tt = torch.arange(t).view(t, 1, 1).expand(t, lh, lw).reshape(-1)
+            hh = torch.arange(lh).view(1, lh, 1).expand(t, lh, lw).reshape(-1)
+            ww = torch.arange(lw).view(1, 1, lw).expand(t, lh, lw).reshape(-1)
+            pos[0, i:j], pos[1, i:j], pos[2, i:j] = tt + cur, hh + cur, ww + cur
+            cur += max(h, w) // spatial_merge_size
+        i = j
+    return pos
+
+
+class QwenVLEncoder:
+    """``Qwen2_5_VLModel`` (vision tower + language model) as the reference's pipeline calls it
+    for prompt embeddings: image embeddings scattered over the ``<|image_pad|>`` tokens, 3-D
+    positions from rope_index, last hidden state after the final norm (hidden_states[-1])."""
+
+    IMAGE_TOKEN_ID = 151655  # <|image_pad|> in the Qwen2.5-VL vocabulary
+
+    def __init__(self, text_config: Optional[TextEncoderConfig] = None, vision_config=None, device="cuda",
+                 image_token_id: int = IMAGE_TOKEN_ID):
+        from .vision import QwenVLVisionTower, VisionConfig
+        self.text = QwenVLTextModel(text_config, device)
+        self.vision = QwenVLVisionTower(vision_config or VisionConfig(), device)
+        if self.vision.config.out_hidden_size != self.text.config.hidden_size:
+            raise ValueError("vision out_hidden_size must equal the text hidden_size")
+        self.image_token_id = image_token_id
+        self.device = self.text.device
+
+    def load_state_dict(self, sd: Dict[str, torch.Tensor]) -> "QwenVLEncoder":
+        self.text.load_state_dict({k: v for k, v in sd.items() if "visual." not in k})
+        self.vision.load_state_dict({k: v for k, v in sd.items() if "visual." in k})
+        return self
+
+    def forward(self, input_ids: torch.Tensor, pixel_values: Optional[torch.Tensor] = None,
+                image_grid_thw=None) -> torch.Tensor:
+        """One prompt: input_ids [S] (or [1, S]) -> hidden states [S, D] bf16."""
+        ids = input_ids.reshape(-1)
+        dev = self.device
+        S = ids.numel()
+        Sp = -(-S // 64) * 64
+        emb = torch.zeros(Sp, self.text.config.hidden_size, dtype=BF16, device=dev)
+        ids_dev = torch.zeros(Sp, dtype=torch.int32, device=dev)
+        ids_dev[:S] = ids.to(dev).to(torch.int32)
+        ops.embed_rows(self.text.w["embed"], ids_dev, out=emb)
+        if pixel_values is not None:
+            img = self.vision(pixel_values, image_grid_thw)
+            where = (ids.cpu() == self.image_token_id).nonzero().view(-1)
+            if where.numel() != img.shape[0]:
+                raise ValueError(f"{where.numel()} image tokens but {img.shape[0]} image embeddings")
+            emb[where.to(dev)] = img  # masked_scatter of the image rows
+        pos = rope_index(ids, self.image_token_id, image_grid_thw if pixel_values is not None else None,
+                         self.vision.config.spatial_merge_size)
+        return self.text(inputs_embeds=emb[:S], position_ids=pos)
+
+    __call__ = forward
+
+
+# ---------------------------------------------------------------------------- pipeline hook
+PROMPT_TEMPLATE = (
+    "<|im_start|>system\nDescribe the key features of the input image (color, shape, size, texture, objects, "
+    "background), then explain how the user's text instruction should alter or modify the image. Generate a new "
+    "image that meets the user's requirements while maintaining consistency with the original input image."
+    "<|im_end|>\n<|im_start|>user\n{}<|im_end|>\n<|im_start|>assistant\n")
+IMAGE_PROMPT_TEMPLATE = "Picture {}: <|vision_start|><|image_pad|><|vision_end|>"
+PROMPT_DROP_TOKENS = 64  # prompt_template_encode_start_idx
+CONDITION_IMAGE_AREA = 384 * 384
+
+
+def condition_size(width: int, height: int, area: int = CONDITION_IMAGE_AREA) -> Tuple[int, int]:
+    """calculate_dimensions(area, w / h): w = sqrt(area r), h = w / r, each rounded to 32."""
+    r = width / height
+    w = math.sqrt(area * r)
+    h = w / r
+    return int(round(w / 32) * 32), int(round(h / 32) * 32)
+
+
+class QwenImageEditPromptEncoder:
+    """``pipe.prompt_encoder`` for QwenImageEditPlusPipeline (encode_prompt's Edit-Plus form,
+    SURVEY.md Appendix A): format the template with one "Picture i" prefix per condition image,
+    run the processor (tokenizer + Qwen2VLImageProcessor, as the reference does -- its vocabulary
+    files come with the checkpoint), encode on the HIP path, drop the first 64 tokens.
+    ``processor(text=[str], images=[PIL...], return_tensors="pt")`` must return input_ids,
+    pixel_values and image_grid_thw (the HF processor's keys)."""
+
+    def __init__(self, encoder: QwenVLEncoder, processor, drop_tokens: int = PROMPT_DROP_TOKENS):
+        self.encoder, self.processor, self.drop = encoder, processor, drop_tokens
+
+    def _condition_images(self, image):
+        if image is None:
+            return []
+        imgs = image if isinstance(image, (list, tuple)) else [image]
+        out = []
+        for im in imgs:
+            if hasattr(im, "resize") and hasattr(im, "size") and not torch.is_tensor(im):
+                w, h = condition_size(*im.size)
+                out.append(im.resize((w, h)))
+            else:
+                out.append(im)
+        return out
+
+    def __call__(self, prompt, image=None):
+        prompts = [prompt] if isinstance(prompt, str) else list(prompt)
+        imgs = self._condition_images(image)
+        prefix = "".join(IMAGE_PROMPT_TEMPLATE.format(i + 1) for i in range(len(imgs)))
+        rows = []
+        for p in prompts:
+            kw = {"images": imgs} if imgs else {}
+            mi = self.processor(text=[PROMPT_TEMPLATE.format(prefix + p)], return_tensors="pt", **kw)
+            ids = mi["input_ids"][0]
+            if "attention_mask" in mi:
+                ids = ids[mi["attention_mask"][0].bool()]
+            h = self.encoder(ids, mi.get("pixel_values"), mi.get("image_grid_thw"))
+            rows.append(h[self.drop:])
+        L = max(r.shape[0] for r in rows)
+        D = rows[0].shape[1]
+        embeds = torch.zeros(len(rows), L, D, dtype=BF16, device=rows[0].device)
+        mask = torch.zeros(len(rows), L, dtype=torch.long, device=rows[0].device)
+        for i, r in enumerate(rows):
+            embeds[i, :r.shape[0]] = r
+            mask[i, :r.shape[0]] = 1
+        return embeds, mask

@@ -3,7 +3,8 @@ and the whole QwenVLTextModel vs transformers' Qwen2_5_VLTextModel (oracle/vl_re
 weights of reduced width, bf16-representable, fp32 eager oracle).
 
 Tolerances:
-  * embed_rows, silu_mul, rope_half: exact vs torch restatements with the same bf16 rounding points
+  * embed_rows, rope_half (bf16 tables): exact vs torch restatements with the same bf16 rounding
+    points; silu_mul, rope_half (fp32 tables), erf GELU: <= 1 bf16 ulp on < 1% of entries
   * causal softmax rows: rel-L2 <= 4e-3, masked entries exactly 0
   * whole text model (2 layers, S = 77 / 128, padded to multiples of 64): rel-L2 <= 2e-2 on the
     last hidden state (every projection re-rounds to bf16; the oracle stays fp32)
@@ -114,3 +115,90 @@ def test_text_model_3d_positions_and_embeds():
     want = VL.text_forward(m, inputs_embeds=emb, position_ids=pos)
     got = te(inputs_embeds=emb.to(DEV), position_ids=pos)
     assert _rel(got, want) <= 2e-2
+
+
+def _vision_cfg():
+    from qwen_image_edit_streamdiffusion_amd.vision import VisionConfig
+    return VisionConfig(depth=4, hidden_size=320, intermediate_size=200, num_heads=4, out_hidden_size=256,
+                        fullatt_block_indexes=(1, 3))
+
+
+def test_rope_half_fp32_tables_slots():
+    """The vision form: fp32 tables, one rounding, 80-wide heads in 128-wide slots."""
+    ops = _ops()
+    g = torch.Generator().manual_seed(6)
+    S, Dh, SL = 50, 80, 128
+    x = torch.randn(S, 4 * SL, generator=g).to(BF16)
+    ang = torch.randn(S, Dh // 2, generator=g)
+    cos, sin = torch.cat([ang.cos(), ang.cos()], -1), torch.cat([ang.sin(), ang.sin()], -1)
+    xd = x.to(DEV)
+    ops.rope_half(xd, 0, 3, Dh, cos.to(DEV), sin.to(DEV), head_stride=SL)
+    q = x.view(S, 4, SL)[:, :3, :Dh].float()
+    rot = torch.cat([-q[..., 40:], q[..., :40]], -1)
+    want = (q * cos[:, None] + rot * sin[:, None]).to(BF16)
+    got = xd.cpu().view(S, 4, SL)
+    d = (got[:, :3, :Dh].float() - want.float()).abs()
+    frac = (d > 0).float().mean().item()
+    # fp32 products / sum then one rounding; v_mul/v_add vs the CPU's vectorised ops may differ in
+    # the last fp32 bit, which moves a rounding tie by one bf16 ulp on a few entries
+    assert (d <= want.float().abs() * 2 ** -7 + 1e-30).all() and frac < 1e-2, (frac, d.max().item())
+    assert torch.equal(got[:, :3, Dh:], x.view(S, 4, SL)[:, :3, Dh:]) and torch.equal(got[:, 3], x.view(S, 4, SL)[:, 3])
+
+
+def test_ranged_softmax_and_gelu_erf():
+    ops = _ops()
+    g = torch.Generator().manual_seed(7)
+    R = 70
+    s = 3 * torch.randn(R, 72, generator=g)
+    cu = [0, 12, 20, 44, 45, 70]  # ragged segments, one of length 1, one unaligned start
+    rng = torch.zeros(R, 2, dtype=torch.int32)
+    for a, b in zip(cu[:-1], cu[1:]):
+        rng[a:b, 0], rng[a:b, 1] = a, b
+    p = torch.full((R, 128), float("nan"), device=DEV).to(BF16)
+    ops.softmax_rows(s.to(DEV), 0.2, out=p, ranges=rng.to(DEV))
+    mask = torch.ones(R, 72, dtype=torch.bool)
+    for a, b in zip(cu[:-1], cu[1:]):
+        mask[a:b, a:b] = False
+    want = torch.softmax((0.2 * s).masked_fill(mask, float("-inf")), -1)
+    got = p.cpu().float()
+    assert _rel(got[:, :72], want) <= 4e-3 and (got[:, :72][mask] == 0).all() and (got[:, 72:] == 0).all()
+    x = (4 * torch.randn(33, 256, generator=g)).to(BF16)
+    y = ops.gelu_erf_(x.to(DEV).clone()).cpu()
+    want = torch.nn.functional.gelu(x.float()).to(BF16)
+    assert ((y.float() - want.float()).abs() <= want.float().abs() * 2 ** -7 + 1e-6).all()
+
+
+@pytest.mark.parametrize("grid", [[(1, 20, 28)], [(1, 16, 16), (1, 8, 12)]])
+def test_vision_tower_vs_transformers(grid):
+    """Patch embed, window permutation, ragged windows, full-attention blocks per image, 2x2 merger."""
+    from oracle import vl_ref as VL
+    from qwen_image_edit_streamdiffusion_amd.vision import QwenVLVisionTower
+    m, sd = VL.tiny_vl_model(1)
+    tower = QwenVLVisionTower(_vision_cfg(), DEV).load_state_dict(sd)
+    S = sum(t * h * w for t, h, w in grid)
+    pv = torch.randn(S, 1176, generator=torch.Generator().manual_seed(S))
+    want = VL.vision_forward(m, pv, torch.tensor(grid))
+    got = tower(pv, grid)
+    assert got.shape == want.shape
+    assert _rel(got, want) <= 2e-2
+
+
+def test_vl_encoder_prompt_with_image_vs_transformers():
+    """Whole Qwen2_5_VLModel: image rows scattered over <|image_pad|>, 3-D positions, hidden_states[-1]."""
+    from oracle import vl_ref as VL
+    from qwen_image_edit_streamdiffusion_amd.text_encoder import QwenVLEncoder, TextEncoderConfig
+    m, sd = VL.tiny_vl_model(2)
+    enc = QwenVLEncoder(TextEncoderConfig(vocab_size=1000, hidden_size=256, intermediate_size=512,
+                                          num_hidden_layers=2, num_attention_heads=2, num_key_value_heads=1),
+                        _vision_cfg(), DEV, image_token_id=990).load_state_dict(sd)
+    g = torch.Generator().manual_seed(8)
+    grid = torch.tensor([[1, 20, 28]])
+    pv = torch.randn(560, 1176, generator=g)
+    ids = torch.cat([torch.randint(0, 900, (70,), generator=g), torch.tensor([992]), torch.full((140,), 990),
+                     torch.tensor([993]), torch.randint(0, 900, (25,), generator=g)])
+    want, _ = VL.vl_forward(m, ids, pv, grid)
+    got = enc(ids, pv, grid)
+    assert got.shape == want.shape and _rel(got, want) <= 2e-2
+    # text-only prompt through the same encoder (the negative / empty-image case)
+    want_t, _ = VL.vl_forward(m, ids[:70])
+    assert _rel(enc(ids[:70]), want_t) <= 2e-2

@@ -39,3 +39,58 @@ def test_text_model_weight_packing_and_config_checks():
     assert torch.equal(L["w_gu"][:512], sd["layers.0.mlp.gate_proj.weight"])
     with pytest.raises(ValueError):
         QwenVLTextModel(TextEncoderConfig(hidden_size=256, num_attention_heads=2, mrope_section=(8, 8, 8)), "cpu")
+
+
+GRIDS = [[(1, 20, 28)], [(1, 16, 16)], [(2, 8, 12)], [(1, 28, 28), (1, 10, 36)]]
+
+
+@pytest.mark.parametrize("grid", GRIDS)
+def test_vision_index_logic_matches_transformers(grid):
+    """Window permutation, window / frame boundaries and (h, w) positions vs transformers.vision_utils."""
+    pytest.importorskip("transformers")
+    from transformers import vision_utils as vu
+    from qwen_image_edit_streamdiffusion_amd.vision import frame_seqlens, vision_position_ids, window_index
+    g = torch.tensor(grid)
+    wi, cu = window_index(grid, 2, 112, 14)
+    wi_ref, cu_ref = vu.get_vision_window_index(g, spatial_merge_size=2, window_size=112, patch_size=14)
+    assert torch.equal(wi, wi_ref) and cu == cu_ref.tolist()
+    assert torch.equal(vision_position_ids(grid, 2), vu.get_vision_position_ids(g, 2))
+    ref = vu.get_vision_cu_seqlens(g).tolist()  # one full-attention block per frame
+    assert frame_seqlens(grid) == ref
+
+
+def test_rope_index_matches_transformers():
+    vl = pytest.importorskip("oracle.vl_ref")
+    from qwen_image_edit_streamdiffusion_amd.text_encoder import rope_index
+    m, _ = vl.tiny_vl_model(0, depth=2, fullatt=(1,))
+    grid = torch.tensor([[1, 20, 28], [1, 8, 12]])
+    ids = torch.cat([torch.arange(5), torch.full((140,), 990), torch.arange(7) + 10, torch.full((24,), 990),
+                     torch.arange(3) + 20]).view(1, -1)
+    want, _ = m.get_rope_index(ids, (ids == 990).int(), image_grid_thw=grid)
+    got = rope_index(ids[0], 990, grid, 2)
+    assert torch.equal(got, want[:, 0])
+    with pytest.raises(ValueError):
+        rope_index(ids[0, :100], 990, grid, 2)
+
+
+def test_condition_size_and_prompt_hook_host():
+    from qwen_image_edit_streamdiffusion_amd.text_encoder import (PROMPT_TEMPLATE, QwenImageEditPromptEncoder,
+                                                                  condition_size)
+    assert condition_size(1024, 1024) == (384, 384)
+    assert condition_size(1920, 1080) == (512, 288)
+    seen = {}
+
+    class Proc:  # records what the hook hands to the processor
+        def __call__(self, text, images=None, return_tensors=None):
+            seen["text"], seen["images"] = text, images
+            return {"input_ids": torch.arange(80).view(1, -1), "attention_mask": torch.ones(1, 80, dtype=torch.long)}
+
+    class Enc:
+        def __call__(self, ids, pv, grid):
+            return torch.arange(ids.numel(), dtype=torch.float).view(-1, 1).expand(-1, 4).to(torch.bfloat16)
+
+    from PIL import Image
+    e, mask = QwenImageEditPromptEncoder(Enc(), Proc())("make it red", Image.new("RGB", (1024, 768)))
+    assert seen["text"] == [PROMPT_TEMPLATE.format("Picture 1: <|vision_start|><|image_pad|><|vision_end|>make it red")]
+    assert seen["images"][0].size == (448, 320)
+    assert e.shape == (1, 16, 4) and e[0, 0, 0].item() == 64 and mask.sum().item() == 16
