@@ -311,9 +311,18 @@ int qie_softmax_rows_f32_bf16(const float* s, int64_t lds, void* p, int64_t ldp,
 /* As qie_softmax_rows_f32_bf16 with row r restricted to keys [ranges[2r], ranges[2r+1]) (device
  * int32 pairs): the vision tower's block-diagonal masks -- windows of cu_window_seqlens and
  * per-image full attention of cu_seqlens (transformers Qwen2_5_VLVisionAttention's per-chunk
- * split). Columns outside the range are written 0 up to ldp. */
+ * split), and (0, r + 1) for the language model's causal mask. Row r uses pair r % period
+ * (head-batched score blocks of `period` rows). Columns outside the range are written 0 up to ldp. */
 int qie_softmax_rows_ranged_f32_bf16(const float* s, int64_t lds, void* p, int64_t ldp, int rows, int N,
-                                     float scale, const int* ranges_dev, qie_stream_t stream);
+                                     float scale, const int* ranges_dev, int period, qie_stream_t stream);
+
+/* Head-batched product (the prompt encoder's attention, all heads in one launch): for z < batch,
+ * y_z = x_z . w_{z / group}^T with x_z = x + z*bsx, w_g = w + g*bsw, y_z = y + z*bsy (elements;
+ * group > 1 = grouped-query attention sharing k / v). out_f32 = 1: raw fp32 [M][N], ldy == N
+ * (scores); out_f32 = 0: bf16(x.w^T + bias) with row stride ldy (P.V into a head's columns). */
+int qie_matmul_batched_bf16(const void* x, int64_t ldx, int64_t bsx, const void* w, int64_t ldw, int64_t bsw,
+                            int group, const void* bias, void* y, int64_t ldy, int64_t bsy, int M, int N, int K,
+                            int batch, int out_f32, qie_stream_t stream);
 
 /* y[c][r] = x[r][c] for an R x C bf16 block (row strides ldx, ldy elements). */
 int qie_transpose_bf16(const void* x, int64_t ldx, void* y, int64_t ldy, int R, int C, qie_stream_t stream);

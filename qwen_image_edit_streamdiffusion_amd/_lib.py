@@ -74,7 +74,8 @@ SIGNATURES = {
     "qie_vae_rgb_in": [P, P, L, P],
     "qie_vae_latents_out_bf16": [P, L, I, I, I, P, P, P, P],
     "qie_embed_rows_bf16": [P, P, I, I, I, P, P],
-    "qie_softmax_rows_ranged_f32_bf16": [P, L, P, L, I, I, F, P, P],
+    "qie_softmax_rows_ranged_f32_bf16": [P, L, P, L, I, I, F, P, I, P],
+    "qie_matmul_batched_bf16": [P, L, L, P, L, L, I, P, P, L, L, I, I, I, I, I, P],
     "qie_rope_half_bf16": [P, L, I, I, I, I, I, P, P, I, P],
     "qie_gelu_erf_bf16": [P, L, I, I, P],
     "qie_silu_mul_bf16": [P, L, I, I, P, L, P],

@@ -55,6 +55,10 @@ struct EpiArgs {
   const float* rsin;
   float eps;
   float qscale;  // EPI_QKV_NR: factor on q (1, or scale*log2(e) for qie_attention_fwd_log2q_bf16)
+  // head-batched products (gemm_kernel, blockIdx.z = batch entry): byte strides of x / w / out,
+  // w advancing once per `group` entries (grouped-query attention shares k / v across a group)
+  int64_t bsx_b, bsw_b, bso_b;
+  int group;
 };
 
 __device__ __forceinline__ int swz_chunk(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
@@ -220,6 +224,12 @@ __global__ void __launch_bounds__(WM* WN * 64)
     gemm_kernel(const char* __restrict__ X, int64_t ldx_b, const char* __restrict__ W, int64_t ldw_b,
                 int M, int N, int K_bytes, EpiArgs e) {
   using Op = MfmaOp<I8>;
+  if (const int bz = blockIdx.z) {  // head-batched launch (gridDim.z == 1 otherwise)
+    X += bz * e.bsx_b;
+    W += (bz / e.group) * e.bsw_b;
+    e.out = (char*)e.out + bz * e.bso_b;
+    e.ws = (char*)e.ws + bz * e.bso_b;
+  }
   constexpr int NWAVE = WM * WN;
   constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int MT = TM / 16, NTL = TN / 16;
@@ -1338,6 +1348,7 @@ EpiArgs make_epi(void* out, int64_t ldo, const void* bias) {
   e.ldo = ldo;
   e.bias = (const bf16_t*)bias;
   e.rows_per_batch = 1;
+  e.group = 1;
   return e;
 }
 
@@ -1584,6 +1595,37 @@ extern "C" int qie_matmul_f32out_bf16(const void* x, int64_t ldx, const void* w,
     const int nwg = ((M + 127) / 128) * ((N + 127) / 128);
     gemm_kernel<128, 128, 2, 2, EPI_PARTIAL, false><<<nwg, 256, 0, s>>>((const char*)x, ldx * 2, (const char*)w,
                                                                         ldw * 2, M, N, kb, e);
+  }
+  return qie_last_error();
+}
+
+// Head-batched product for the prompt encoder's attention: for z < batch,
+//   y_z = x_z . w_{z / group}^T   (x_z = x + z bsx, w_g = w + g bsw, y_z = y + z bsy; elements)
+// out_f32 = 1: raw fp32 [M][N] (ldy == N) -- the scores; out_f32 = 0: bf16(x.w^T + bias) with
+// row stride ldy -- P.V into each head's column slice.
+extern "C" int qie_matmul_batched_bf16(const void* x, int64_t ldx, int64_t bsx, const void* w, int64_t ldw,
+                                       int64_t bsw, int group, const void* bias, void* y, int64_t ldy, int64_t bsy,
+                                       int M, int N, int K, int batch, int out_f32, qie_stream_t stream) {
+  QIE_CHECK_ARG(x && w && y && M > 0 && N > 0 && K > 0 && K % 64 == 0 && N % 4 == 0 && batch > 0 && group > 0);
+  QIE_CHECK_ARG(batch <= 65535 && ldx % 8 == 0 && ldw % 8 == 0 && bsx % 8 == 0 && bsw % 8 == 0);
+  QIE_CHECK_ARG(((uintptr_t)x % 16) == 0 && ((uintptr_t)w % 16) == 0);
+  EpiArgs e = make_epi(y, ldy, bias);
+  e.bsx_b = bsx * 2;
+  e.bsw_b = bsw * 2;
+  e.group = group;
+  const dim3 grid(((M + 127) / 128) * ((N + 127) / 128), 1, batch);
+  const hipStream_t s = (hipStream_t)stream;
+  if (out_f32) {
+    QIE_CHECK_ARG(ldy == N && ((uintptr_t)y % 16) == 0 && bsy % 4 == 0);
+    e.ws = y;
+    e.bso_b = bsy * 4;
+    gemm_kernel<128, 128, 2, 2, EPI_PARTIAL, false><<<grid, 256, 0, s>>>((const char*)x, ldx * 2, (const char*)w,
+                                                                         ldw * 2, M, N, K * 2, e);
+  } else {
+    QIE_CHECK_ARG(bias && ldy % 4 == 0 && ((uintptr_t)y % 8) == 0 && bsy % 4 == 0);
+    e.bso_b = bsy * 2;
+    gemm_kernel<128, 128, 2, 2, EPI_BIAS, false><<<grid, 256, 0, s>>>((const char*)x, ldx * 2, (const char*)w,
+                                                                      ldw * 2, M, N, K * 2, e);
   }
   return qie_last_error();
 }

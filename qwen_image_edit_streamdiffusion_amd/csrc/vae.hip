@@ -105,15 +105,16 @@ __device__ __forceinline__ void ml_merge(float& m, float& l, float m2, float l2)
 
 __global__ void __launch_bounds__(256)
     softmax_rows_kernel(const float* __restrict__ s, int64_t lds, bf16_t* __restrict__ p, int64_t ldp, int Nall,
-                        float scale, int causal, const int* __restrict__ ranges) {
+                        float scale, int causal, const int* __restrict__ ranges, int period) {
   const int64_t row = blockIdx.x;
+  const int rr = (int)(row % period);  // row within its head (head-batched score blocks)
   // Keys [c0, c1) of row r: all Nall; causal (the text encoder's decoder mask) 0..r; ranges (the
   // vision tower's window / per-image blocks) ranges[2r] .. ranges[2r+1]. Other columns are 0.
   int c0 = 0, c1 = Nall;
-  if (causal) c1 = min(Nall, (int)row + 1);
+  if (causal) c1 = min(Nall, rr + 1);
   if (ranges) {
-    c0 = max(ranges[2 * row], 0);
-    c1 = min(ranges[2 * row + 1], Nall);
+    c0 = max(ranges[2 * rr], 0);
+    c1 = min(ranges[2 * rr + 1], Nall);
   }
   const float* sr = s + row * lds;
   __shared__ float red_m[4], red_l[4];
@@ -255,15 +256,18 @@ extern "C" int qie_softmax_rows_f32_bf16(const float* s, int64_t lds, void* p, i
                                          float scale, int causal, qie_stream_t stream) {
   QIE_CHECK_ARG(s && p && rows > 0 && N > 0 && N % 4 == 0 && lds >= N && lds % 4 == 0);
   QIE_CHECK_ARG(ldp >= N && ldp % 4 == 0 && ((uintptr_t)s % 16) == 0 && ((uintptr_t)p % 8) == 0);
-  softmax_rows_kernel<<<rows, 256, 0, (hipStream_t)stream>>>(s, lds, (bf16_t*)p, ldp, N, scale, causal, nullptr);
+  softmax_rows_kernel<<<rows, 256, 0, (hipStream_t)stream>>>(s, lds, (bf16_t*)p, ldp, N, scale, causal, nullptr,
+                                                              rows);
   return qie_last_error();
 }
 
 extern "C" int qie_softmax_rows_ranged_f32_bf16(const float* s, int64_t lds, void* p, int64_t ldp, int rows, int N,
-                                                float scale, const int* ranges_dev, qie_stream_t stream) {
+                                                float scale, const int* ranges_dev, int period, qie_stream_t stream) {
   QIE_CHECK_ARG(s && p && ranges_dev && rows > 0 && N > 0 && N % 4 == 0 && lds >= N && lds % 4 == 0);
+  QIE_CHECK_ARG(period > 0 && rows % period == 0);
   QIE_CHECK_ARG(ldp >= N && ldp % 4 == 0 && ((uintptr_t)s % 16) == 0 && ((uintptr_t)p % 8) == 0);
-  softmax_rows_kernel<<<rows, 256, 0, (hipStream_t)stream>>>(s, lds, (bf16_t*)p, ldp, N, scale, 0, ranges_dev);
+  softmax_rows_kernel<<<rows, 256, 0, (hipStream_t)stream>>>(s, lds, (bf16_t*)p, ldp, N, scale, 0, ranges_dev,
+                                                              period);
   return qie_last_error();
 }
 

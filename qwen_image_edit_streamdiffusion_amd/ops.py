@@ -478,7 +478,8 @@ def softmax_rows(s: torch.Tensor, scale: float, out: Optional[torch.Tensor] = No
                  causal: bool = False, ranges: Optional[torch.Tensor] = None) -> torch.Tensor:
     """bf16 softmax(scale * s) per row of fp32 s [R, N]; ``out`` [R, >=N] (contiguous; columns past
     N -- the K padding of a following GEMM -- are zero-filled). ``causal``: row r keeps columns
-    0..r; ``ranges`` (device int32 [R, 2]): row r keeps columns [ranges[r, 0], ranges[r, 1])."""
+    0..r; ``ranges`` (device int32 [P, 2], R % P == 0): row r keeps columns [ranges[r % P, 0],
+    ranges[r % P, 1]) -- P rows per head when R stacks the score blocks of several heads."""
     _dev(s, out, ranges)
     _chk(s.dtype == torch.float32 and _is2d_rowmajor(s), "fp32 [rows, N]")
     R, N = s.shape
@@ -486,13 +487,46 @@ def softmax_rows(s: torch.Tensor, scale: float, out: Optional[torch.Tensor] = No
         out = torch.empty(R, N, dtype=BF16, device=s.device)
     _chk(out.is_contiguous() and out.shape[0] == R and out.shape[1] >= N and out.dtype == BF16, "out")
     if ranges is not None:
-        _chk(not causal and ranges.dtype == torch.int32 and ranges.is_contiguous() and ranges.shape == (R, 2),
-             "ranges int32 [rows, 2]")
+        P = ranges.shape[0]
+        _chk(not causal and ranges.dtype == torch.int32 and ranges.is_contiguous() and ranges.shape == (P, 2)
+             and R % P == 0, "ranges int32 [period, 2], rows % period == 0")
         _lib.call("qie_softmax_rows_ranged_f32_bf16", _p(s), s.stride(0), _p(out), out.shape[1], R, N, scale,
-                  _p(ranges), _stream())
+                  _p(ranges), P, _stream())
     else:
         _lib.call("qie_softmax_rows_f32_bf16", _p(s), s.stride(0), _p(out), out.shape[1], R, N, scale,
                   int(causal), _stream())
+    return out
+
+
+def _span_ok(t: torch.Tensor, batch: int, bs: int) -> bool:
+    """The last batch entry of a 2-D row-major view stays inside its storage."""
+    R, C = t.shape
+    end = t.storage_offset() + (batch - 1) * bs + (R - 1) * t.stride(0) + C
+    return end * t.element_size() <= t.untyped_storage().nbytes()
+
+
+def matmul_heads(x: torch.Tensor, bsx: int, w: torch.Tensor, bsw: int, out: torch.Tensor, bsy: int, batch: int,
+                 group: int = 1, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Head-batched x_z . w_{z // group}^T for z < batch: x / w / out are the views of entry 0
+    (row-major, [M, K] / [N, K] / [M, N]) and bs* the element strides between entries. fp32 out:
+    raw scores (contiguous rows, ldy == N); bf16 out: bf16(x.w^T + bias)."""
+    _dev(x, w, out, bias)
+    _chk(x.dtype == BF16 and w.dtype == BF16 and _is2d_rowmajor(x) and _is2d_rowmajor(w) and _is2d_rowmajor(out),
+         "bf16 row-major operands")
+    M, K = x.shape
+    N = w.shape[0]
+    _chk(w.shape[1] == K and out.shape == (M, N) and batch >= 1 and group >= 1, "shapes")
+    _chk(K % 64 == 0 and N % 4 == 0, "K % 64 == 0 and N % 4 == 0 required")
+    _chk(_span_ok(x, batch, bsx) and _span_ok(w, -(-batch // group), bsw) and _span_ok(out, batch, bsy),
+         "batched views exceed their storage")
+    f32 = out.dtype == torch.float32
+    if f32:
+        _chk(out.stride(0) == N, "fp32 scores need ldy == N")
+    else:
+        _chk(out.dtype == BF16 and bias is not None and bias.numel() == N and bias.dtype == BF16, "bf16 out + bias")
+    _lib.call("qie_matmul_batched_bf16", _p(x), x.stride(0), bsx, _p(w), w.stride(0), bsw, group,
+              _p(bias) if bias is not None else None, _p(out), out.stride(0), bsy, M, N, K, batch, int(f32),
+              _stream())
     return out
 
 

@@ -14,15 +14,17 @@ FlowMatch schedule, and the denoise loop with **batched CFG** (a3, the absent
 batch axis in ONE forward, unequal text lengths key-masked so the result equals
 the reference's two sequential forwards), the true-CFG norm rescale (a2) and
 the Euler step, then the VAE decode (§8 f1, ``vae.QwenImageVAEDecoder``: unpack,
-de-normalise, decoder, uint8 RGB, all on the HIP path).  The text encoder
-(Qwen2.5-VL, §8 f2) and the VAE *encoder* are still "next": callers pass
-``prompt_embeds`` / ``image_latents`` directly or plug encoders in through the
-``prompt_encoder`` / ``image_encoder`` hooks (``latent_decoder`` overrides the
-HIP decoder).  ``output_type="latent"`` returns packed latents, as diffusers does.
+de-normalise, decoder, uint8 RGB, all on the HIP path).  The condition image is
+VAE-encoded on the HIP path (``vae.QwenImageVAEEncoder``) and the prompt is encoded
+by Qwen2.5-VL on the HIP path (§8 f2, ``text_encoder.QwenImageEditPromptEncoder``
+behind the snapshot's processor); callers may still pass ``prompt_embeds`` /
+``image_latents`` directly or plug their own encoders into the ``prompt_encoder`` /
+``image_encoder`` hooks (``latent_decoder`` overrides the HIP decoder).  ``output_type="latent"`` returns packed latents, as diffusers does.
 """
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 from typing import Any, Callable, List, Optional, Sequence, Tuple
 
@@ -135,7 +137,20 @@ class QwenImageEditPlusPipeline:
         elif random_init_seed is not None or path is None:
             pipe.vae = QwenImageVAEDecoder(device=device).random_init_(seed=(random_init_seed or 0) + 1)
             pipe.vae_encoder = QwenImageVAEEncoder(device=device).random_init_(seed=(random_init_seed or 0) + 2)
+        if path is not None and os.path.isdir(os.path.join(path, "text_encoder")):
+            pipe.prompt_encoder = cls._snapshot_prompt_encoder(path, device)
         return pipe
+
+    @staticmethod
+    def _snapshot_prompt_encoder(path: str, device):
+        """The snapshot's Qwen2.5-VL on the HIP path behind the snapshot's own processor
+        (``processor/``: tokenizer + Qwen2VLImageProcessor, loaded from local files only)."""
+        from transformers import AutoProcessor
+        from .text_encoder import QwenImageEditPromptEncoder
+        proc_dir = os.path.join(path, "processor")
+        processor = AutoProcessor.from_pretrained(proc_dir if os.path.isdir(proc_dir) else path,
+                                                  local_files_only=True)
+        return QwenImageEditPromptEncoder(W.load_prompt_encoder(path, device=device), processor)
 
     def to(self, device=None, *a, **k):
         return self
@@ -155,8 +170,8 @@ class QwenImageEditPlusPipeline:
         if embeds is None:
             if self.prompt_encoder is None:
                 raise NotImplementedError(
-                    "prompt text encoding (Qwen2.5-VL, SURVEY.md §8 f2) is not on the HIP hot path yet: "
-                    "pass prompt_embeds= or set pipe.prompt_encoder")
+                    "no prompt encoder: load a snapshot with text_encoder/ + processor/, set pipe.prompt_encoder "
+                    "(text_encoder.QwenImageEditPromptEncoder), or pass prompt_embeds=")
             embeds, mask = self.prompt_encoder(prompt, image)
         if mask is None:
             mask = torch.ones(embeds.shape[:2], dtype=torch.long, device=embeds.device)

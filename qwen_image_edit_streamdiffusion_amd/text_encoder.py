@@ -12,8 +12,9 @@ that turns the condition image into the ``<|image_pad|>`` embeddings is the next
 
 MI355X mapping: every projection is one GEMM (q|k|v packed, gate|up packed; o_proj and down_proj
 carry the residual add in their epilogue), RMSNorm / RoPE / SwiGLU / embedding are HIP kernels,
-attention is per query head: fp32 scores by GEMM, causal softmax, P.V by GEMM against V^T (prompt
-lengths are a few hundred tokens; the GQA group shares its V^T).
+attention runs all heads per launch: head-batched fp32 score GEMM (GQA: the kv operand advances once
+per group), one causal softmax over every head's rows, head-batched P.V against V^T (prompt
+lengths are a few hundred tokens, so the full score blocks stay small).
 """
 from __future__ import annotations
 
@@ -65,6 +66,38 @@ def mrope_tables(cfg: TextEncoderConfig, position_ids: torch.Tensor) -> Tuple[to
         parts_s.append(sin[i % 3, :, o:o + n])
         o += n
     return torch.cat(parts_c, -1).to(BF16), torch.cat(parts_s, -1).to(BF16)
+
+
+def text_state_dict_shapes(c: TextEncoderConfig) -> Dict[str, Tuple[int, ...]]:
+    """Qwen2_5_VLTextModel parameter names (text-model relative) and shapes."""
+    D, F, Dh = c.hidden_size, c.intermediate_size, c.head_dim
+    kv = c.num_key_value_heads * Dh
+    out = {"embed_tokens.weight": (c.vocab_size, D), "norm.weight": (D,)}
+    for i in range(c.num_hidden_layers):
+        p = f"layers.{i}."
+        out.update({p + "input_layernorm.weight": (D,), p + "post_attention_layernorm.weight": (D,),
+                    p + "self_attn.q_proj.weight": (D, D), p + "self_attn.q_proj.bias": (D,),
+                    p + "self_attn.k_proj.weight": (kv, D), p + "self_attn.k_proj.bias": (kv,),
+                    p + "self_attn.v_proj.weight": (kv, D), p + "self_attn.v_proj.bias": (kv,),
+                    p + "self_attn.o_proj.weight": (D, D), p + "mlp.gate_proj.weight": (F, D),
+                    p + "mlp.up_proj.weight": (F, D), p + "mlp.down_proj.weight": (D, F)})
+    return out
+
+
+def random_state_dict(shapes: Dict[str, Tuple[int, ...]], device, seed: int = 0) -> Dict[str, torch.Tensor]:
+    """Random-init bf16 weights generated on ``device`` (the checkpoint is not available offline):
+    norms ~1, biases ~0.02, matrices ~N(0, 1/fan_in)."""
+    g = torch.Generator(device=device).manual_seed(seed)
+    sd = {}
+    for k, s in shapes.items():
+        if k.endswith("norm.weight") or "norm" in k.split(".")[-2] or "ln_q" in k:
+            t = torch.ones(s, device=device)
+        elif k.endswith("bias"):
+            t = 0.02 * torch.randn(s, generator=g, device=device)
+        else:
+            t = torch.randn(s, generator=g, device=device) / math.sqrt(math.prod(s[1:]))
+        sd[k] = t.to(BF16)
+    return sd
 
 
 class QwenVLTextModel:
@@ -142,23 +175,24 @@ class QwenVLTextModel:
         h = torch.empty(Sp, D, dtype=BF16, device=dev)
         qkv = torch.empty(Sp, (H + 2 * Hk) * Dh, dtype=BF16, device=dev)
         att = torch.empty(Sp, H * Dh, dtype=BF16, device=dev)
-        s = torch.empty(Sp, Sp, dtype=torch.float32, device=dev)
-        p = torch.empty(Sp, Sp, dtype=BF16, device=dev)
-        vt = torch.empty(Dh, Sp, dtype=BF16, device=dev)
+        s = torch.empty(H * Sp, Sp, dtype=torch.float32, device=dev)  # all heads' scores
+        p = torch.empty(H * Sp, Sp, dtype=BF16, device=dev)
+        vt = torch.empty(Hk * Dh, Sp, dtype=BF16, device=dev)
+        causal = torch.stack([torch.zeros(Sp, dtype=torch.int32), torch.arange(1, Sp + 1, dtype=torch.int32)], 1)
+        causal = causal.to(dev)
         gu = torch.empty(Sp, 2 * F, dtype=BF16, device=dev)
         a = torch.empty(Sp, F, dtype=BF16, device=dev)
         scale = 1.0 / math.sqrt(Dh)
+        G = H // Hk  # query heads per kv head
         for L in self.layers:
             ops.rmsnorm(x, L["ln1"], out=h, eps=c.rms_norm_eps)
             ops.linear(h, L["w_qkv"], L["b_qkv"], out=qkv)
             ops.rope_half(qkv, 0, H + Hk, Dh, cos, sin)  # q heads, then the k heads right after them
-            for kv in range(Hk):
-                k = qkv[:, (H + kv) * Dh:(H + kv + 1) * Dh]
-                ops.transpose(qkv[:, (H + Hk + kv) * Dh:(H + Hk + kv + 1) * Dh], out=vt)
-                for hq in range(kv * (H // Hk), (kv + 1) * (H // Hk)):
-                    ops.matmul_f32out(qkv[:, hq * Dh:(hq + 1) * Dh], k, out=s)
-                    ops.softmax_rows(s, scale, out=p, causal=True)
-                    ops.linear(p, vt, w["zero_hd"], out=att[:, hq * Dh:(hq + 1) * Dh])
+            ops.transpose(qkv[:, (H + Hk) * Dh:], out=vt)  # V^T of every kv head
+            # every head in one launch per step: scores, causal softmax, P.V (kv head = q head // G)
+            ops.matmul_heads(qkv[:, :Dh], Dh, qkv[:, H * Dh:(H + 1) * Dh], Dh, s[:Sp], Sp * Sp, H, group=G)
+            ops.softmax_rows(s, scale, out=p, ranges=causal)
+            ops.matmul_heads(p[:Sp], Sp * Sp, vt[:Dh], Dh * Sp, att[:, :Dh], Dh, H, group=G, bias=w["zero_hd"])
             ops.linear_gated_residual(att, L["w_o"], w["zero_d"], w["ones"], Sp, x)
             ops.rmsnorm(x, L["ln2"], out=h, eps=c.rms_norm_eps)
             ops.linear(h, L["w_gu"], w["zero_2f"], out=gu)

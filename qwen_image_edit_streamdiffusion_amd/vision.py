@@ -12,8 +12,9 @@ replace the ``<|image_pad|>`` tokens of the prompt (text_encoder.QwenVLEncoder).
 
 MI355X mapping: every linear is one GEMM; the 80-wide heads sit in 128-wide zero-padded slots
 (the fp32 score GEMM needs K % 64; zeros leave q.k and P.V unchanged) and the SwiGLU width 3420 is
-zero-padded to 3456, both once at load time. Attention is per head: fp32 scores for all rows by
-GEMM, a softmax that keeps each row's window (or image) range, P.V by GEMM against V^T. The
+zero-padded to 3456, both once at load time. Attention runs all heads per launch: head-batched fp32
+score GEMM over all rows, one softmax that keeps each row's window (or image) range, head-batched
+P.V against V^T. The
 window permutation and its inverse are row gathers (the embedding kernel).
 """
 from __future__ import annotations
@@ -57,6 +58,22 @@ class VisionConfig:
     @property
     def patch_dim(self) -> int:
         return self.in_channels * self.temporal_patch_size * self.patch_size ** 2
+
+
+def vision_state_dict_shapes(c: VisionConfig) -> Dict[str, Tuple[int, ...]]:
+    """Qwen2_5_VisionTransformerPretrainedModel parameter names (tower relative) and shapes."""
+    D, F, m = c.hidden_size, c.intermediate_size, c.spatial_merge_size ** 2
+    out = {"patch_embed.proj.weight": (D, c.in_channels, c.temporal_patch_size, c.patch_size, c.patch_size),
+           "merger.ln_q.weight": (D,), "merger.mlp.0.weight": (m * D, m * D), "merger.mlp.0.bias": (m * D,),
+           "merger.mlp.2.weight": (c.out_hidden_size, m * D), "merger.mlp.2.bias": (c.out_hidden_size,)}
+    for i in range(c.depth):
+        p = f"blocks.{i}."
+        out.update({p + "norm1.weight": (D,), p + "norm2.weight": (D,), p + "attn.qkv.weight": (3 * D, D),
+                    p + "attn.qkv.bias": (3 * D,), p + "attn.proj.weight": (D, D), p + "attn.proj.bias": (D,),
+                    p + "mlp.gate_proj.weight": (F, D), p + "mlp.gate_proj.bias": (F,),
+                    p + "mlp.up_proj.weight": (F, D), p + "mlp.up_proj.bias": (F,),
+                    p + "mlp.down_proj.weight": (D, F), p + "mlp.down_proj.bias": (D,)})
+    return out
 
 
 # ---------------------------------------------------------------------------- host index logic
@@ -229,9 +246,9 @@ class QwenVLVisionTower:
         h = torch.empty(Sp, D, dtype=BF16, device=dev)
         qkv = torch.empty(Sp, 3 * H * SL, dtype=BF16, device=dev)
         att = torch.empty(Sp, H * SL, dtype=BF16, device=dev)
-        s = torch.empty(Sp, Sp, dtype=torch.float32, device=dev)
-        p = torch.empty(Sp, Sp, dtype=BF16, device=dev)
-        vt = torch.empty(SL, Sp, dtype=BF16, device=dev)
+        s = torch.empty(H * Sp, Sp, dtype=torch.float32, device=dev)  # all heads' scores
+        p = torch.empty(H * Sp, Sp, dtype=BF16, device=dev)
+        vt = torch.empty(H * SL, Sp, dtype=BF16, device=dev)
         gu = torch.empty(Sp, 2 * self.Fp, dtype=BF16, device=dev)
         a = torch.empty(Sp, self.Fp, dtype=BF16, device=dev)
         scale = Dh ** -0.5
@@ -240,13 +257,10 @@ class QwenVLVisionTower:
             ops.rmsnorm(x, B["n1"], out=h, eps=c.rms_norm_eps)
             ops.linear(h, B["w_qkv"], B["b_qkv"], out=qkv)
             ops.rope_half(qkv, 0, 2 * H, Dh, cos, sin, head_stride=SL)
-            for hd in range(H):
-                q = qkv[:, hd * SL:(hd + 1) * SL]
-                k = qkv[:, (H + hd) * SL:(H + hd + 1) * SL]
-                ops.transpose(qkv[:, (2 * H + hd) * SL:(2 * H + hd + 1) * SL], out=vt)
-                ops.matmul_f32out(q, k, out=s)
-                ops.softmax_rows(s, scale, out=p, ranges=rng)
-                ops.linear(p, vt, w["zero_slot"], out=att[:, hd * SL:(hd + 1) * SL])
+            ops.transpose(qkv[:, 2 * H * SL:], out=vt)
+            ops.matmul_heads(qkv[:, :SL], SL, qkv[:, H * SL:(H + 1) * SL], SL, s[:Sp], Sp * Sp, H)
+            ops.softmax_rows(s, scale, out=p, ranges=rng)
+            ops.matmul_heads(p[:Sp], Sp * Sp, vt[:SL], SL * Sp, att[:, :SL], SL, H, bias=w["zero_slot"])
             ops.linear_gated_residual(att, B["w_proj"], B["b_proj"], w["ones"], Sp, x)
             ops.rmsnorm(x, B["n2"], out=h, eps=c.rms_norm_eps)
             ops.linear(h, B["w_gu"], B["b_gu"], out=gu)

@@ -235,3 +235,58 @@ def load_vae_encoder(path: str, device="cuda"):
     from .vae import QwenImageVAEEncoder
     return QwenImageVAEEncoder(_vae_config(path), device).load_state_dict(
         _vae_tensors(path, ("encoder.", "quant_conv.")))
+
+
+# ---------------------------------------------------------------------------- prompt encoder (§8 f2)
+def _prompt_encoder_configs(path: str):
+    """(TextEncoderConfig, VisionConfig, image_token_id) from ``text_encoder/config.json`` -- the
+    Qwen2_5_VLConfig of the snapshot; text fields at the top level (transformers 4.x checkpoints)
+    or under ``text_config``."""
+    import json
+    from .text_encoder import QwenVLEncoder, TextEncoderConfig
+    from .vision import VisionConfig
+    tc, vc, img = TextEncoderConfig(), VisionConfig(), QwenVLEncoder.IMAGE_TOKEN_ID
+    cj = os.path.join(path, "text_encoder", "config.json")
+    if os.path.isfile(cj):
+        with open(cj) as fh:
+            c = json.load(fh)
+        t = dict(c)
+        t.update(c.get("text_config") or {})
+        for k in ("vocab_size", "hidden_size", "intermediate_size", "num_hidden_layers", "num_attention_heads",
+                  "num_key_value_heads"):
+            if k in t:
+                setattr(tc, k, int(t[k]))
+        if "rms_norm_eps" in t:
+            tc.rms_norm_eps = float(t["rms_norm_eps"])
+        rope = t.get("rope_parameters") or t.get("rope_scaling") or {}
+        if "rope_theta" in t or "rope_theta" in rope:
+            tc.rope_theta = float(rope.get("rope_theta", t.get("rope_theta")))
+        if "mrope_section" in rope:
+            tc.mrope_section = tuple(int(v) for v in rope["mrope_section"])
+        v = c.get("vision_config") or {}
+        for k in ("depth", "hidden_size", "intermediate_size", "num_heads", "in_channels", "patch_size",
+                  "temporal_patch_size", "spatial_merge_size", "window_size", "out_hidden_size"):
+            if k in v:
+                setattr(vc, k, int(v[k]))
+        if "fullatt_block_indexes" in v:
+            vc.fullatt_block_indexes = tuple(int(i) for i in v["fullatt_block_indexes"])
+        img = int(c.get("image_token_id", img))
+    return tc, vc, img
+
+
+def load_prompt_encoder(path: str, device="cuda"):
+    """QwenVLEncoder (Qwen2.5-VL vision tower + language model) from a diffusers snapshot's
+    ``text_encoder/`` (config.json + safetensors shards; ``lm_head`` is skipped unread)."""
+    from safetensors import safe_open
+    from .text_encoder import QwenVLEncoder
+    files = sorted(glob.glob(os.path.join(path, "text_encoder", "*.safetensors"))) if os.path.isdir(path) else []
+    if not files:
+        raise FileNotFoundError(f"no text_encoder/*.safetensors under {path}")
+    tc, vc, img = _prompt_encoder_configs(path)
+    sd = {}
+    for f in files:
+        with safe_open(f, framework="pt", device="cpu") as fh:
+            for k in fh.keys():
+                if not k.startswith("lm_head"):
+                    sd[k] = fh.get_tensor(k)
+    return QwenVLEncoder(tc, vc, device, image_token_id=img).load_state_dict(sd)

@@ -162,6 +162,12 @@ def test_ranged_softmax_and_gelu_erf():
     want = torch.softmax((0.2 * s).masked_fill(mask, float("-inf")), -1)
     got = p.cpu().float()
     assert _rel(got[:, :72], want) <= 4e-3 and (got[:, :72][mask] == 0).all() and (got[:, 72:] == 0).all()
+    # head-batched: three heads' score blocks share the per-row ranges (period R)
+    s3 = 3 * torch.randn(3 * R, 72, generator=g)
+    p3 = torch.empty(3 * R, 72, dtype=BF16, device=DEV)
+    ops.softmax_rows(s3.to(DEV), 0.2, out=p3, ranges=rng.to(DEV))
+    want3 = torch.softmax((0.2 * s3).masked_fill(mask.repeat(3, 1), float("-inf")), -1)
+    assert _rel(p3, want3) <= 4e-3
     x = (4 * torch.randn(33, 256, generator=g)).to(BF16)
     y = ops.gelu_erf_(x.to(DEV).clone()).cpu()
     want = torch.nn.functional.gelu(x.float()).to(BF16)
@@ -202,3 +208,29 @@ def test_vl_encoder_prompt_with_image_vs_transformers():
     # text-only prompt through the same encoder (the negative / empty-image case)
     want_t, _ = VL.vl_forward(m, ids[:70])
     assert _rel(enc(ids[:70]), want_t) <= 2e-2
+
+
+@pytest.mark.parametrize("group", [1, 7])
+def test_matmul_heads_batched(group):
+    """Head-batched products on strided column slices (GQA: the w operand advances per group)."""
+    ops = _ops()
+    g = torch.Generator().manual_seed(9)
+    S, Dh, H = 192, 128, 14  # S is the P.V reduction length: a multiple of 64 (the models pad)
+    Hk = H // group
+    qkv = torch.randn(S, (H + 2 * Hk) * Dh, generator=g).to(BF16).to(DEV)
+    s = torch.empty(H * S, S, dtype=torch.float32, device=DEV)
+    ops.matmul_heads(qkv[:, :Dh], Dh, qkv[:, H * Dh:(H + 1) * Dh], Dh, s[:S], S * S, H, group=group)
+    q = qkv[:, :H * Dh].float().cpu().view(S, H, Dh)
+    k = qkv[:, H * Dh:(H + Hk) * Dh].float().cpu().view(S, Hk, Dh)
+    want = torch.einsum("shd,thd->hst", q, k.repeat_interleave(group, 1)).reshape(H * S, S)
+    assert _rel(s, want) <= 1e-5
+    p = torch.randn(H * S, S, generator=g).to(BF16).to(DEV)
+    vt = torch.randn(Hk * Dh, S, generator=g).to(BF16).to(DEV)
+    out = torch.empty(S, H * Dh, dtype=BF16, device=DEV)
+    bias = torch.zeros(Dh, dtype=BF16, device=DEV)
+    ops.matmul_heads(p[:S], S * S, vt[:Dh], Dh * S, out[:, :Dh], Dh, H, group=group, bias=bias)
+    pv = torch.einsum("hst,hdt->shd", p.float().cpu().view(H, S, S),
+                      vt.float().cpu().view(Hk, Dh, S).repeat_interleave(group, 0)).reshape(S, H * Dh)
+    assert _rel(out, pv) <= 4e-3
+    with pytest.raises(ValueError):  # the last head would run past the buffer
+        ops.matmul_heads(qkv[:, :Dh], Dh, qkv[:, H * Dh:(H + 1) * Dh], Dh, s[:S], S * S, H + 1, group=group)

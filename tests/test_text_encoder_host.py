@@ -94,3 +94,43 @@ def test_condition_size_and_prompt_hook_host():
     assert seen["text"] == [PROMPT_TEMPLATE.format("Picture 1: <|vision_start|><|image_pad|><|vision_end|>make it red")]
     assert seen["images"][0].size == (448, 320)
     assert e.shape == (1, 16, 4) and e[0, 0, 0].item() == 64 and mask.sum().item() == 16
+
+
+def test_state_dict_shapes_match_transformers():
+    vl = pytest.importorskip("oracle.vl_ref")
+    from qwen_image_edit_streamdiffusion_amd.text_encoder import text_state_dict_shapes
+    from qwen_image_edit_streamdiffusion_amd.vision import VisionConfig, vision_state_dict_shapes
+    _, sd = vl.tiny_vl_model(0)
+    tc = TextEncoderConfig(vocab_size=1000, hidden_size=256, intermediate_size=512, num_hidden_layers=2,
+                           num_attention_heads=2, num_key_value_heads=1)
+    vc = VisionConfig(depth=4, hidden_size=320, intermediate_size=200, num_heads=4, out_hidden_size=256)
+    want = {k: tuple(v.shape) for k, v in sd.items()}
+    got = {"language_model." + k: v for k, v in text_state_dict_shapes(tc).items()}
+    got.update({"visual." + k: v for k, v in vision_state_dict_shapes(vc).items()})
+    assert got == want
+
+
+def test_load_prompt_encoder_from_snapshot(tmp_path):
+    """text_encoder/config.json + safetensors (transformers 4.x key layout, lm_head present) -> the
+    encoder's configs and packed weights (loaded on the CPU; the forward needs the GPU)."""
+    import json
+    from safetensors.torch import save_file
+    vl = pytest.importorskip("oracle.vl_ref")
+    from qwen_image_edit_streamdiffusion_amd.weights import load_prompt_encoder
+    m, sd = vl.tiny_vl_model(3)
+    d = tmp_path / "text_encoder"
+    d.mkdir()
+    old = {("model." + k[len("language_model."):] if k.startswith("language_model.") else k): v.contiguous()
+           for k, v in sd.items()}
+    old["lm_head.weight"] = torch.zeros(1000, 256, dtype=BF16)
+    save_file(old, str(d / "model.safetensors"))
+    cfg = m.config.to_dict()
+    tcd = cfg.pop("text_config")
+    cfg.update(tcd)  # 4.x layout: text fields at the top level
+    (d / "config.json").write_text(json.dumps(cfg))
+    enc = load_prompt_encoder(str(tmp_path), device="cpu")
+    assert enc.text.config.hidden_size == 256 and enc.text.config.num_key_value_heads == 1
+    assert enc.vision.config.hidden_size == 320 and enc.vision.config.fullatt_block_indexes == (1, 3)
+    assert enc.vision.config.intermediate_size == 200 and enc.image_token_id == 990
+    assert torch.equal(enc.text.w["embed"], sd["language_model.embed_tokens.weight"])
+    assert torch.equal(enc.vision.blocks[1]["w_down"][:, :200], sd["visual.blocks.1.mlp.down_proj.weight"])
