@@ -147,8 +147,9 @@ def load_pipeline_from_env(device: str = "cuda"):
     ``QIE_MODEL_PATH``: diffusers snapshot or pre-quantised int8 image (weights.save_int8);
     ``QIE_LORA_PATH`` [+ ``QIE_LORA_WEIGHT``]: Lightning LoRA, fused at load;
     ``QIE_INT8=1``: quantise the linears (W8A8) after loading;
-    ``QIE_ENCODERS=module:factory``: ``factory(pipeline)`` sets ``prompt_encoder`` /
-    ``image_encoder`` / ``latent_decoder`` (the Qwen2.5-VL text encoder and the VAE, §8 f1/f2).
+    ``QIE_ENCODERS=module:factory``: ``factory(pipeline)`` overrides ``prompt_encoder`` /
+    ``image_encoder`` / ``latent_decoder``. By default the snapshot's own VAE (``vae/``) and
+    Qwen2.5-VL prompt encoder (``text_encoder/`` + ``processor/``) run on the HIP path (§8 f1/f2).
     """
     from .pipeline import QwenImageEditPlusPipeline
     path = os.environ.get("QIE_MODEL_PATH")

@@ -22,6 +22,7 @@ N-step denoise of that frame (tests/test_gpu_pipeline.py checks this).
 """
 from __future__ import annotations
 
+import os
 import time
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Tuple
@@ -233,7 +234,18 @@ class QwenRealtimePipeline:
 
     def load_model(self, transformer: Optional[QwenImageTransformer2DModel] = None, seed: int = 0,
                    vae=None, **config_overrides):
-        """``vae``: a QwenImageVAEDecoder, or "random" for a seeded random one (benchmarks)."""
+        """``vae``: a QwenImageVAEDecoder, or "random" for a seeded random one (benchmarks).
+        Without a transformer, ``config.model_name`` naming a local diffusers snapshot loads
+        everything from it as qwen_realtime.py:116-122 does -- DiT, VAE encoder / decoder and the
+        Qwen2.5-VL prompt encoder, all on the HIP path; otherwise a seeded random DiT."""
+        if transformer is None and os.path.isdir(self.config.model_name):
+            from .pipeline import QwenImageEditPlusPipeline
+            pipe = QwenImageEditPlusPipeline.from_pretrained(self.config.model_name, torch_dtype=self.config.dtype)
+            transformer = pipe.transformer
+            if vae is None and pipe.vae is not None:
+                vae = (pipe.vae, pipe.vae_encoder)
+            if self.prompt_encoder is None:
+                self.prompt_encoder = pipe.prompt_encoder
         if transformer is None:
             transformer = QwenImageTransformer2DModel(**config_overrides).random_init_(seed)
         self.transformer = transformer
@@ -254,7 +266,8 @@ class QwenRealtimePipeline:
             return
         if prompt_embeds is None:
             if self.prompt_encoder is None:
-                raise NotImplementedError("pass prompt_embeds= (text encoder is SURVEY.md §8 f2)")
+                raise NotImplementedError("no prompt encoder: load_model() from a local snapshot with "
+                                          "text_encoder/ + processor/, pass prompt_encoder=, or prompt_embeds=")
             prompt_embeds, prompt_embeds_mask = self.prompt_encoder(prompt, reference_image)
             if self.config.true_cfg_scale > 1:
                 negative_prompt_embeds, negative_prompt_embeds_mask = self.prompt_encoder(" ", reference_image)
