@@ -100,6 +100,50 @@ def random_state_dict(shapes: Dict[str, Tuple[int, ...]], device, seed: int = 0)
     return sd
 
 
+def encoder_splits(M: int, N: int, K: int) -> int:
+    """K ranges for an encoder linear: prompts are a few hundred rows, so a projection with a
+    narrow N (o_proj, down_proj, the vision proj / down) fills only a fraction of the 256 CUs
+    with 256x256 tiles; split K until tiles x splits reaches about one round, >= 8 K tiles each."""
+    tiles = -(-M // 256) * -(-N // 256)
+    steps = K * 2 // 128
+    for sp in range(min(256 // tiles, steps // 8), 1, -1):
+        if steps % sp == 0:
+            return sp
+    return 1
+
+
+class EncoderLinears:
+    """The encoders' projections: split-K (fp32 partials in a shared workspace, reduced in range
+    order with the real epilogue) where encoder_splits says the unsplit grid is too small, the
+    plain GEMM otherwise."""
+
+    def __init__(self, device):
+        self.device = device
+        self.ws = torch.empty(0, dtype=torch.float32, device=device)
+
+    def _workspace(self, M, N, sp):
+        need = ops.splitk_workspace_bytes(M, N, sp) // 4
+        if self.ws.numel() < need:
+            self.ws = torch.empty(need, dtype=torch.float32, device=self.device)
+        return self.ws
+
+    def linear(self, x, w, b, out):
+        M, K = x.shape
+        sp = encoder_splits(M, w.shape[0], K)
+        if sp == 1:
+            return ops.linear(x, w, b, out=out)
+        return ops.linear_splitk(x, w, b, ops.EPI_BIAS, out, self._workspace(M, w.shape[0], sp), sp)
+
+    def residual(self, x, w, b, ones, resid):
+        """resid += x.w^T + b (the gated-residual epilogue with a unit gate)."""
+        M, K = x.shape
+        sp = encoder_splits(M, w.shape[0], K)
+        if sp == 1:
+            return ops.linear_gated_residual(x, w, b, ones, M, resid)
+        return ops.linear_splitk(x, w, b, ops.EPI_GATED_RESIDUAL, resid, self._workspace(M, w.shape[0], sp), sp,
+                                 gate=ones, rows_per_batch=M)
+
+
 class QwenVLTextModel:
     """``Qwen2_5_VLTextModel`` forward on the HIP path (one prompt at a time: no padding mask)."""
 
@@ -113,6 +157,7 @@ class QwenVLTextModel:
             raise ValueError("mrope_section must cover head_dim / 2")
         self.layers: List[Dict[str, torch.Tensor]] = []
         self.w: Dict[str, torch.Tensor] = {}
+        self.lin = EncoderLinears(self.device)
 
     # ------------------------------------------------------------------ weights
     @staticmethod
@@ -186,18 +231,18 @@ class QwenVLTextModel:
         G = H // Hk  # query heads per kv head
         for L in self.layers:
             ops.rmsnorm(x, L["ln1"], out=h, eps=c.rms_norm_eps)
-            ops.linear(h, L["w_qkv"], L["b_qkv"], out=qkv)
+            self.lin.linear(h, L["w_qkv"], L["b_qkv"], qkv)
             ops.rope_half(qkv, 0, H + Hk, Dh, cos, sin)  # q heads, then the k heads right after them
             ops.transpose(qkv[:, (H + Hk) * Dh:], out=vt)  # V^T of every kv head
             # every head in one launch per step: scores, causal softmax, P.V (kv head = q head // G)
             ops.matmul_heads(qkv[:, :Dh], Dh, qkv[:, H * Dh:(H + 1) * Dh], Dh, s[:Sp], Sp * Sp, H, group=G)
             ops.softmax_rows(s, scale, out=p, ranges=causal)
             ops.matmul_heads(p[:Sp], Sp * Sp, vt[:Dh], Dh * Sp, att[:, :Dh], Dh, H, group=G, bias=w["zero_hd"])
-            ops.linear_gated_residual(att, L["w_o"], w["zero_d"], w["ones"], Sp, x)
+            self.lin.residual(att, L["w_o"], w["zero_d"], w["ones"], x)
             ops.rmsnorm(x, L["ln2"], out=h, eps=c.rms_norm_eps)
-            ops.linear(h, L["w_gu"], w["zero_2f"], out=gu)
+            self.lin.linear(h, L["w_gu"], w["zero_2f"], gu)
             ops.silu_mul(gu, out=a)
-            ops.linear_gated_residual(a, L["w_down"], w["zero_d"], w["ones"], Sp, x)
+            self.lin.residual(a, L["w_down"], w["zero_d"], w["ones"], x)
         ops.rmsnorm(x, w["norm"], out=h, eps=c.rms_norm_eps)
         return h[:S]
 

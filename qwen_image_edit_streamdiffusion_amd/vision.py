@@ -166,6 +166,8 @@ class QwenVLVisionTower:
         self.Kp = _ru(c.patch_dim, 64)
         self.blocks: List[Dict[str, torch.Tensor]] = []
         self.w: Dict[str, torch.Tensor] = {}
+        from .text_encoder import EncoderLinears
+        self.lin = EncoderLinears(self.device)
 
     @staticmethod
     def _strip(sd):
@@ -255,22 +257,23 @@ class QwenVLVisionTower:
         for i, B in enumerate(self.blocks):
             rng = rng_full if i in c.fullatt_block_indexes else rng_win
             ops.rmsnorm(x, B["n1"], out=h, eps=c.rms_norm_eps)
-            ops.linear(h, B["w_qkv"], B["b_qkv"], out=qkv)
+            self.lin.linear(h, B["w_qkv"], B["b_qkv"], qkv)
             ops.rope_half(qkv, 0, 2 * H, Dh, cos, sin, head_stride=SL)
             ops.transpose(qkv[:, 2 * H * SL:], out=vt)
             ops.matmul_heads(qkv[:, :SL], SL, qkv[:, H * SL:(H + 1) * SL], SL, s[:Sp], Sp * Sp, H)
             ops.softmax_rows(s, scale, out=p, ranges=rng)
             ops.matmul_heads(p[:Sp], Sp * Sp, vt[:SL], SL * Sp, att[:, :SL], SL, H, bias=w["zero_slot"])
-            ops.linear_gated_residual(att, B["w_proj"], B["b_proj"], w["ones"], Sp, x)
+            self.lin.residual(att, B["w_proj"], B["b_proj"], w["ones"], x)
             ops.rmsnorm(x, B["n2"], out=h, eps=c.rms_norm_eps)
-            ops.linear(h, B["w_gu"], B["b_gu"], out=gu)
+            self.lin.linear(h, B["w_gu"], B["b_gu"], gu)
             ops.silu_mul(gu, out=a)
-            ops.linear_gated_residual(a, B["w_down"], B["b_down"], w["ones"], Sp, x)
+            self.lin.residual(a, B["w_down"], B["b_down"], w["ones"], x)
         ops.rmsnorm(x, w["ln_q"], out=h, eps=c.rms_norm_eps)
         hm = h.view(Sp // unit, unit * D)
-        m1 = ops.linear(hm, w["m0_w"], w["m0_b"])
+        m1 = self.lin.linear(hm, w["m0_w"], w["m0_b"], torch.empty(Sp // unit, unit * D, dtype=BF16, device=dev))
         ops.gelu_erf_(m1)
-        m2 = ops.linear(m1, w["m2_w"], w["m2_b"])
+        m2 = self.lin.linear(m1, w["m2_w"], w["m2_b"],
+                             torch.empty(Sp // unit, c.out_hidden_size, dtype=BF16, device=dev))
         out = torch.empty(S // unit, c.out_hidden_size, dtype=BF16, device=dev)
         ops.embed_rows(m2, inv_dev, out=out)  # back to raster (merge-block) order
         return out

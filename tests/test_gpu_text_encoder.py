@@ -234,3 +234,22 @@ def test_matmul_heads_batched(group):
     assert _rel(out, pv) <= 4e-3
     with pytest.raises(ValueError):  # the last head would run past the buffer
         ops.matmul_heads(qkv[:, :Dh], Dh, qkv[:, H * Dh:(H + 1) * Dh], Dh, s[:S], S * S, H + 1, group=group)
+
+
+def test_encoder_linears_splitk():
+    """The encoders' split-K projections (plain and residual) vs fp32 torch on the same operands."""
+    from qwen_image_edit_streamdiffusion_amd.text_encoder import EncoderLinears, encoder_splits
+    g = torch.Generator().manual_seed(10)
+    M, N, K = 320, 512, 2048
+    assert encoder_splits(M, N, K) > 1
+    x = torch.randn(M, K, generator=g).to(BF16)
+    w = (torch.randn(N, K, generator=g) / K ** 0.5).to(BF16)
+    b = (0.1 * torch.randn(N, generator=g)).to(BF16)
+    lin = EncoderLinears(torch.device(DEV))
+    out = lin.linear(x.to(DEV), w.to(DEV), b.to(DEV), torch.empty(M, N, dtype=BF16, device=DEV))
+    want = x.float() @ w.float().T + b.float()
+    assert _rel(out, want) <= 4e-3
+    r = torch.randn(M, N, generator=g).to(BF16)
+    rd = r.to(DEV)
+    lin.residual(x.to(DEV), w.to(DEV), b.to(DEV), torch.ones(1, N, dtype=BF16, device=DEV), rd)
+    assert _rel(rd, r.float() + want) <= 4e-3
