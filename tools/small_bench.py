@@ -1,0 +1,48 @@
+"""Time the DiT's bandwidth-bound small kernels at the bench shapes (B = 2 stream batch):
+modulation GEMV (M = 2, N = 6 D, K = D), LayerNorm + modulate on the image rows."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from qwen_image_edit_streamdiffusion_amd import ops  # noqa: E402
+
+
+def bench(fn, it=50):
+    for _ in range(5):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(it):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / it * 1e3
+
+
+dev = "cuda"
+D = 3072
+x = torch.randn(2, D, device=dev).to(torch.bfloat16)
+w = (torch.randn(6 * D, D, device=dev) / 60).to(torch.bfloat16)
+b = torch.zeros(6 * D, device=dev, dtype=torch.bfloat16)
+out = torch.empty(2, 6 * D, device=dev, dtype=torch.bfloat16)
+t = bench(lambda: ops.gemv(x, w, b, out=out))
+print(f"gemv M=2 N={6 * D} K={D}: {t:.1f} us, {w.numel() * 2 / t / 1e6:.2f} TB/s")
+if len(sys.argv) > 1:  # A/B against another build's gemv: python tools/small_bench.py other.so
+    import ctypes
+    lib = ctypes.CDLL(sys.argv[1])
+    lib.qie_gemv_bf16.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
+                                  ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                  ctypes.c_void_p]
+    st = torch.cuda.current_stream().cuda_stream
+    t2 = bench(lambda: lib.qie_gemv_bf16(x.data_ptr(), D, w.data_ptr(), b.data_ptr(), out.data_ptr(), 6 * D,
+                                         2, 6 * D, D, st))
+    print(f"  {sys.argv[1]}: {t2:.1f} us, {w.numel() * 2 / t2 / 1e6:.2f} TB/s")
+R = 2 * 8192
+h = torch.randn(R, D, device=dev).to(torch.bfloat16)
+mod = torch.randn(2, 6 * D, device=dev).to(torch.bfloat16)
+o = torch.empty_like(h)
+t = bench(lambda: ops.layernorm_modulate(h, mod[:, :D], mod[:, D:2 * D], 8192, out=o))
+print(f"ln_mod rows={R} D={D}: {t:.1f} us, {2 * h.numel() * 2 / t / 1e6:.2f} TB/s")
