@@ -112,6 +112,19 @@ __device__ __forceinline__ void attn_dma(const i32x4_t& r, const char QIE_LDS* d
       : "v"(voff), "s"(r), "s"(lds), "s"(soff)
       : "memory");
 }
+#ifndef QIE_ATTN_LEAN  // 1: DMA pieces without the hand-saved M0 / leading s_nop (M0 declared clobbered)
+#define QIE_ATTN_LEAN 1
+#endif
+__device__ __forceinline__ void attn_dma_lean(const i32x4_t& r, const char QIE_LDS* dst, uint32_t voff, int soff) {
+  const int lds = __builtin_amdgcn_readfirstlane((int)(uint32_t)(uintptr_t)dst);
+  asm volatile(
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %0, %1, %3 offen lds"
+      :
+      : "v"(voff), "s"(r), "s"(lds), "s"(soff)
+      : "memory", "m0");
+}
 __device__ __forceinline__ void mma32(f32x16_t& c, const bf16x8_t& a, const bf16x8_t& b) {
   asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(c) : "v"(a), "v"(b));
 }
@@ -207,12 +220,18 @@ __global__ void __launch_bounds__(512) attn_pp_kernel(AttnArgs a) {
   auto dmaK = [&](int t) {
     char QIE_LDS* base = smem + (t % kRing) * kTileBytes;
 #pragma unroll
-    for (int p = 0; p < 2; ++p) attn_dma(kr, base + (wave + 8 * p) * 1024, ko[p], t * kTileBytes);
+    for (int p = 0; p < 2; ++p) {
+      if constexpr (QIE_ATTN_LEAN) attn_dma_lean(kr, base + (wave + 8 * p) * 1024, ko[p], t * kTileBytes);
+      else attn_dma(kr, base + (wave + 8 * p) * 1024, ko[p], t * kTileBytes);
+    }
   };
   auto dmaV = [&](int t) {
     char QIE_LDS* base = smem + (kRing + t % kRing) * kTileBytes;
 #pragma unroll
-    for (int p = 0; p < 2; ++p) attn_dma(vr, base + (wave + 8 * p) * 1024, vo[p], t * kTileBytes);
+    for (int p = 0; p < 2; ++p) {
+      if constexpr (QIE_ATTN_LEAN) attn_dma_lean(vr, base + (wave + 8 * p) * 1024, vo[p], t * kTileBytes);
+      else attn_dma(vr, base + (wave + 8 * p) * 1024, vo[p], t * kTileBytes);
+    }
   };
 
   // per-lane LDS read offsets (K: chunk ^ (row & 15); V: transposed 4x16 reads, chunk ^ ((row & 3) << 2))

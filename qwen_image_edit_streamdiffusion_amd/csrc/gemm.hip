@@ -360,6 +360,21 @@ constexpr int k4Slots = kRingD + 1;     // LDS ring slots (4: 128 KiB, 5: 160 Ki
 #define QIE_RING_NT 4
 #endif
 constexpr int kRingNT = QIE_RING_NT;
+#ifndef QIE_PP_LEAN  // gemm_pp: DMA pieces through pp_dma_lean (no hand-saved M0, no leading s_nop): +2-4 % A/B
+#define QIE_PP_LEAN 1
+#endif
+#ifndef QIE_W4_LEAN  // gemm_w4: 1 = DMA pieces without the hand-saved M0 / leading s_nop (pp_dma_lean)
+#define QIE_W4_LEAN 1
+#endif
+#ifndef QIE_W4_ABL  // timing ablations of gemm_w4 (wrong results): 1 no DMA in the loop, 2 no vmcnt at the barrier
+#define QIE_W4_ABL 0
+#endif
+#ifndef QIE_W4_DMA  // gemm_w4: where the 16 DMA pieces of tile k+2 go in stage B (see the kernel)
+#define QIE_W4_DMA 1
+#endif
+#ifndef QIE_GEMM_W4  // 1: gemm_w4_kernel (4 waves of 128x128) for the big plain / GELU / residual shapes
+#define QIE_GEMM_W4 0
+#endif
 #ifndef QIE_GEMM_PP  // 1: gemm_pp_kernel for the big shapes (+14 % over gemm_ring in A/B); 0: gemm_ring
 #define QIE_GEMM_PP 1
 #endif
@@ -825,6 +840,19 @@ __device__ __forceinline__ void pp_dma(const i32x4_t& r, const char QIE_LDS* dst
       : "memory");
 }
 
+// the same piece for a loop where every operand is SALU-computed (no fresh readfirstlane): no
+// leading s_nop, and M0 declared clobbered instead of saved / restored by hand
+__device__ __forceinline__ void pp_dma_lean(const i32x4_t& r, const char QIE_LDS* dst, uint32_t voff, int soff) {
+  const int lds = __builtin_amdgcn_readfirstlane((int)(uint32_t)(uintptr_t)dst);
+  asm volatile(
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %0, %1, %3 offen lds"
+      :
+      : "v"(voff), "s"(r), "s"(lds), "s"(soff)
+      : "memory", "m0");
+}
+
 constexpr int kPPTile = 256 * kRowBytes;  // one operand of one K tile, 32 KiB
 #ifndef QIE_PP_XRING  // X tiles in flight + 1: 2 -> 128 KiB of LDS, 3 -> all 160 KiB
 #define QIE_PP_XRING 2
@@ -874,8 +902,14 @@ __global__ void __launch_bounds__(512, 2)
   // LDS: X slots [0, kPPX) (tile kt in slot kt % kPPX), then two W slots (tile kt in kt & 1)
   auto xslot = [&](int kt) { return smem + (kt % kPPX) * kPPTile; };
   auto wslot = [&](int kt) { return smem + (kPPX + (kt & 1)) * kPPTile; };
-  auto dmaX = [&](int kt, int i) { pp_dma(xr, xslot(kt) + (wave + i * NWAVE) * 1024, xo[i], kt * kRowBytes); };
-  auto dmaW = [&](int kt, int i) { pp_dma(wr, wslot(kt) + (wave + i * NWAVE) * 1024, wo[i], kt * kRowBytes); };
+  auto dmaX = [&](int kt, int i) {
+    if constexpr (QIE_PP_LEAN) pp_dma_lean(xr, xslot(kt) + (wave + i * NWAVE) * 1024, xo[i], kt * kRowBytes);
+    else pp_dma(xr, xslot(kt) + (wave + i * NWAVE) * 1024, xo[i], kt * kRowBytes);
+  };
+  auto dmaW = [&](int kt, int i) {
+    if constexpr (QIE_PP_LEAN) pp_dma_lean(wr, wslot(kt) + (wave + i * NWAVE) * 1024, wo[i], kt * kRowBytes);
+    else pp_dma(wr, wslot(kt) + (wave + i * NWAVE) * 1024, wo[i], kt * kRowBytes);
+  };
 
   // fragment of k-step ks: lane reads row (lane & 15) of its 16-row block, chunk 4 ks + (lane >> 4)
   const int fr = lane & 15;
@@ -985,6 +1019,154 @@ __global__ void __launch_bounds__(512, 2)
   ring_epilogue<NT, EPI, I8>(acc, e, M, N, m0 + wm * 128, n0 + wn * NT * 16, lane, smem);
 }
 
+// ---------------------------------------------------------------------------------------------
+// gemm_w4: the 256x256 tile as FOUR waves of 128x128 -- one wave per SIMD, 8x8 16x16 MFMA tiles
+// = 256 AGPR accumulators -- on the 64-wide K tiles of 128-byte LDS rows that gemm_pp uses.
+// Why (profiles/r07_gemm_vs_hipblaslt_pmc.json): the library kernel with this shape runs one
+// wave per SIMD that is parked 6 % of its cycles and reads 1/3 less LDS per MFMA (128x128 wave
+// tile: 16 fragments per 64 MFMAs instead of 12 per 32), where gemm_pp's two ping-pong waves
+// park 31 %. Per K tile (two k-steps, 128 MFMAs per wave):
+//   stage A: 64 MFMAs of k-step 0 (fragment set 0), the k-step 1 fragments of the same tile read
+//            into set 1 between them (one ds_read_b128 per 4 MFMAs);
+//   barrier: vmcnt(0) lgkmcnt(0) -> this wave's DMA pieces of tile k+1 have landed and its reads
+//            of tile k have retired; after the barrier that holds for every wave, so
+//   stage B: 64 MFMAs of k-step 1 (set 1), the k-step 0 fragments of tile k+1 read into set 0
+//            and the 16 DMA pieces of tile k+2 issued into tile k's slot (one per 4 MFMAs).
+// Two slots of [X 256 rows | W 256 rows] x 128 B = 128 KiB; one barrier per 128 MFMAs.
+template <int EPI, bool I8>
+__global__ void __launch_bounds__(256, 1)
+    gemm_w4_kernel(const char* __restrict__ X, int64_t ldx_b, const char* __restrict__ W, int64_t ldw_b,
+                   int M, int N, int K_bytes, EpiArgs e) {
+  using frag = typename MfmaOp<I8>::frag;
+  using accT = typename MfmaOp<I8>::acc;
+  constexpr int NWAVE = 4, PPO = 8;  // PPO: DMA pieces per wave per operand tile (32 pieces / 4 waves)
+  __shared__ __attribute__((aligned(16))) char smem_raw[4 * kPPTile];
+  char QIE_LDS* smem = (char QIE_LDS*)smem_raw;
+
+  const int tiles_m = (M + 255) >> 8, tiles_n = (N + 255) >> 8;
+  const int nwg = tiles_m * tiles_n;
+  const int wgid = xcd_remap(blockIdx.x, nwg);
+  constexpr int GROUP = 8;
+  const int per_group = GROUP * tiles_n;
+  const int first_m = (wgid / per_group) * GROUP;
+  const int gsz = min(tiles_m - first_m, GROUP);
+  const int tm = first_m + (wgid % per_group) % gsz;
+  const int tn = (wgid % per_group) / gsz;
+  const int m0 = tm * 256, n0 = tn * 256;
+
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int m_valid = M - m0, n_valid = N - n0;
+  const int nk = K_bytes / kRowBytes;  // host guarantees nk >= 3
+
+  const int64_t koff = (int64_t)blockIdx.y * K_bytes;  // split-K range (gridDim.y == 1 otherwise)
+  const i32x4_t xr = pp_rsrc(X + (int64_t)m0 * ldx_b + koff, (int)(min(m_valid, 256) * ldx_b - koff));
+  const i32x4_t wr = pp_rsrc(W + (int64_t)n0 * ldw_b + koff, (int)(min(n_valid, 256) * ldw_b - koff));
+  // piece i of an operand tile: rows 8 (wave + 4 i) .. +7, lane -> row + (lane >> 3), swizzled chunk
+  uint32_t xo[PPO], wo[PPO];
+#pragma unroll
+  for (int i = 0; i < PPO; ++i) {
+    const int r = (wave + i * NWAVE) * 8 + (lane >> 3);
+    const int c = swz_chunk(r, lane & 7);
+    xo[i] = (uint32_t)(min(r, m_valid - 1) * ldx_b) + (c << 4);
+    wo[i] = (uint32_t)(min(r, n_valid - 1) * ldw_b) + (c << 4);
+  }
+  // slot s = kt & 1: X tile at s * 2 * kPPTile, W tile right after it
+  auto xslot = [&](int kt) { return smem + (kt & 1) * 2 * kPPTile; };
+  auto wslot = [&](int kt) { return smem + (kt & 1) * 2 * kPPTile + kPPTile; };
+  // DMA piece p (0..15) of tile kt: p < 8 -> X piece p, else W piece p - 8
+  auto dma = [&](int kt, int p) {
+    if constexpr (QIE_W4_LEAN) {
+      if (p < PPO) pp_dma_lean(xr, xslot(kt) + (wave + p * NWAVE) * 1024, xo[p], kt * kRowBytes);
+      else pp_dma_lean(wr, wslot(kt) + (wave + (p - PPO) * NWAVE) * 1024, wo[p - PPO], kt * kRowBytes);
+    } else {
+      if (p < PPO) pp_dma(xr, xslot(kt) + (wave + p * NWAVE) * 1024, xo[p], kt * kRowBytes);
+      else pp_dma(wr, wslot(kt) + (wave + (p - PPO) * NWAVE) * 1024, wo[p - PPO], kt * kRowBytes);
+    }
+  };
+
+  const int fr = lane & 15;
+  const int sw = (fr >> 1) & 7;
+  const int a_row = wm * 128 + fr, w_row = wn * 128 + fr;
+  // fragment r (0..15) of k-step ks of tile kt: r < 8 -> W rows w_row + 16 r, else X rows a_row + 16 (r - 8)
+  auto ldfrag = [&](int kt, int ks, int r) -> frag {
+    const int cofs = ((4 * ks + (lane >> 4)) ^ sw) << 4;
+    if (r < 8) return *(const frag QIE_LDS*)(wslot(kt) + (w_row + 16 * r) * kRowBytes + cofs);
+    return *(const frag QIE_LDS*)(xslot(kt) + (a_row + 16 * (r - 8)) * kRowBytes + cofs);
+  };
+
+  accT acc[8][8];
+  frag wf[2][8], af[2][8];
+
+  // one k-step: 64 MFMAs on set CUR (row i = q / 8, column tile j = q % 8); RD: read k-step
+  // (rkt, rks) into set CUR ^ 1 (fragment q / 4 after MFMA q, q % 4 == 1); DM: DMA tile dkt
+  // (piece q / 4 after MFMA q, q % 4 == 3)
+  auto kstep = [&](auto cur_t, auto init_t, auto rd_t, auto dm_t, int rkt, int rks, int dkt) {
+    constexpr int CUR = decltype(cur_t)::value;
+    constexpr bool INIT = decltype(init_t)::value, RD = decltype(rd_t)::value, DM = decltype(dm_t)::value;
+#pragma unroll
+    for (int q = 0; q < 64; ++q) {
+      const int i = q >> 3, j = q & 7;
+      if constexpr (INIT) Mma4<I8>::init(acc[i][j], wf[CUR][j], af[CUR][i]);
+      else Mma4<I8>::acc(acc[i][j], wf[CUR][j], af[CUR][i]);
+      if constexpr (RD) {
+        if ((q & 3) == 1) {
+          const int r = q >> 2;
+          if (r < 8) wf[CUR ^ 1][r] = ldfrag(rkt, rks, r);
+          else af[CUR ^ 1][r - 8] = ldfrag(rkt, rks, r);
+        }
+      }
+      if constexpr (DM && !(QIE_W4_ABL & 1)) {  // QIE_W4_DMA: 0 spread (1 per 4 MFMAs), 1 burst (1 per MFMA), 2 (1 per 2)
+        if constexpr (QIE_W4_DMA == 0) {
+          if ((q & 3) == 3) dma(dkt, q >> 2);
+        } else if constexpr (QIE_W4_DMA == 1) {
+          if (q < 16) dma(dkt, q);
+        } else {
+          if ((q & 1) == 1 && q < 32) dma(dkt, q >> 1);
+        }
+      }
+    }
+  };
+  using T = std::true_type;
+  using F = std::false_type;
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  auto bar = [&]() {
+    if constexpr (QIE_W4_ABL & 2) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // timing only
+    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  };
+
+  // prologue: tiles 0 and 1 in flight, tile 0 landed, its k-step 0 fragments read
+#pragma unroll
+  for (int p = 0; p < 2 * PPO; ++p) dma(0, p);
+#pragma unroll
+  for (int p = 0; p < 2 * PPO; ++p) dma(1, p);
+  asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
+#pragma unroll
+  for (int r = 0; r < 8; ++r) wf[0][r] = ldfrag(0, 0, r);
+#pragma unroll
+  for (int r = 0; r < 8; ++r) af[0][r] = ldfrag(0, 0, 8 + r);
+
+  // tile 0 (INIT), tiles 1 .. nk-3 (steady), nk-2 (no DMA), nk-1 (no reads ahead)
+  kstep(I0{}, T{}, T{}, F{}, 0, 1, 0);
+  bar();
+  kstep(I1{}, F{}, T{}, T{}, 1, 0, 2);
+  int kt = 1;
+  for (; kt < nk - 2; ++kt) {
+    kstep(I0{}, F{}, T{}, F{}, kt, 1, 0);
+    bar();
+    kstep(I1{}, F{}, T{}, T{}, kt + 1, 0, kt + 2);
+  }
+  kstep(I0{}, F{}, T{}, F{}, kt, 1, 0);  // nk-2
+  bar();
+  kstep(I1{}, F{}, T{}, F{}, kt + 1, 0, 0);
+  kstep(I0{}, F{}, T{}, F{}, kt + 1, 1, 0);  // nk-1
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  kstep(I1{}, F{}, F{}, F{}, 0, 0, 0);
+
+  ring_epilogue<8, EPI, I8>(acc, e, M, N, m0 + wm * 128, n0 + wn * 128, lane, smem);
+}
+
 template <int EPI, bool I8>
 int launch_gemm(const void* x, int64_t ldx, const void* w, int64_t ldw, int M, int N, int K,
                 const EpiArgs& e, hipStream_t s) {
@@ -1001,7 +1183,10 @@ int launch_gemm(const void* x, int64_t ldx, const void* w, int64_t ldw, int M, i
                     (EPI != EPI_GATE_RES || (((uintptr_t)e.gate % 16) == 0 && e.gate_bstride % 8 == 0)) &&
                     (EPI != EPI_QKV || e.head_dim % 8 == 0);
   if (wide && M >= 256 && N >= 256 && big_tiles >= 160 && kb >= (kRingD + 2) * k4RowBytes) {
-    if constexpr (QIE_GEMM_PP)  // (kb % 128 == 0 and kb >= 320 hold, so nk >= 3)
+    if constexpr (QIE_GEMM_W4 && EPI != EPI_QKV_NR)
+      gemm_w4_kernel<EPI, I8><<<(int)big_tiles, 256, 0, s>>>((const char*)x, ldx_b, (const char*)w, ldw_b, M, N,
+                                                            kb, e);
+    else if constexpr (QIE_GEMM_PP)  // (kb % 128 == 0 and kb >= 320 hold, so nk >= 3)
       gemm_pp_kernel<EPI, I8><<<(int)big_tiles, 512, 0, s>>>((const char*)x, ldx_b, (const char*)w, ldw_b, M,
                                                             N, kb, e);
     else
