@@ -366,13 +366,13 @@ constexpr int kRingNT = QIE_RING_NT;
 #ifndef QIE_W4_LEAN  // gemm_w4: 1 = DMA pieces without the hand-saved M0 / leading s_nop (pp_dma_lean)
 #define QIE_W4_LEAN 1
 #endif
-#ifndef QIE_W4_ABL  // timing ablations of gemm_w4 (wrong results): 1 no DMA in the loop, 2 no vmcnt at the barrier
+#ifndef QIE_W4_ABL  // timing ablations of gemm_w4 (wrong results): 1 no DMA in the loop, 2 no vmcnt at the barrier, 4 (w4s) loads from tile 0 only
 #define QIE_W4_ABL 0
 #endif
 #ifndef QIE_W4_DMA  // gemm_w4: where the 16 DMA pieces of tile k+2 go in stage B (see the kernel)
 #define QIE_W4_DMA 1
 #endif
-#ifndef QIE_GEMM_W4  // 1: gemm_w4_kernel (4 waves of 128x128) for the big plain / GELU / residual shapes
+#ifndef QIE_GEMM_W4  // big plain / GELU / residual shapes: 1 gemm_w4_kernel (4 waves of 128x128, LDS-DMA), 2 gemm_w4s_kernel (VGPR-staged)
 #define QIE_GEMM_W4 0
 #endif
 #ifndef QIE_GEMM_PP  // 1: gemm_pp_kernel for the big shapes (+14 % over gemm_ring in A/B); 0: gemm_ring
@@ -1167,6 +1167,157 @@ __global__ void __launch_bounds__(256, 1)
   ring_epilogue<8, EPI, I8>(acc, e, M, N, m0 + wm * 128, n0 + wn * 128, lane, smem);
 }
 
+// gemm_w4s: gemm_w4 with the operand tiles staged through VGPRs instead of LDS-DMA (the
+// library's form): every thread loads its 16 x 16 B of tile k+3 with buffer_load_dwordx4 (64
+// VGPRs) while tile k computes, and writes tile k+2 from the registers into the slot freed by
+// the mid-tile barrier. The LDS layout (128-byte rows, XOR-swizzled chunks) is gemm_w4's; the
+// ablation there showed the DMA issue itself as the cost (0.80 ms without it vs 0.93 ms).
+template <int EPI, bool I8>
+__global__ void __launch_bounds__(256, 1)
+    gemm_w4s_kernel(const char* __restrict__ X, int64_t ldx_b, const char* __restrict__ W, int64_t ldw_b,
+                    int M, int N, int K_bytes, EpiArgs e) {
+  using frag = typename MfmaOp<I8>::frag;
+  using accT = typename MfmaOp<I8>::acc;
+  typedef unsigned int g4_t __attribute__((ext_vector_type(4)));
+  constexpr int NWAVE = 4, PPO = 8;
+  __shared__ __attribute__((aligned(16))) char smem_raw[4 * kPPTile];
+  char QIE_LDS* smem = (char QIE_LDS*)smem_raw;
+
+  const int tiles_m = (M + 255) >> 8, tiles_n = (N + 255) >> 8;
+  const int nwg = tiles_m * tiles_n;
+  const int wgid = xcd_remap(blockIdx.x, nwg);
+  constexpr int GROUP = 8;
+  const int per_group = GROUP * tiles_n;
+  const int first_m = (wgid / per_group) * GROUP;
+  const int gsz = min(tiles_m - first_m, GROUP);
+  const int tm = first_m + (wgid % per_group) % gsz;
+  const int tn = (wgid % per_group) / gsz;
+  const int m0 = tm * 256, n0 = tn * 256;
+
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int m_valid = M - m0, n_valid = N - n0;
+  const int nk = K_bytes / kRowBytes;  // host guarantees nk >= 3
+
+  const int64_t koff = (int64_t)blockIdx.y * K_bytes;
+  auto mk = [](const char* base, int bytes) {
+    const uint64_t p = (uint64_t)base;
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)p);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(p >> 32));
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0,
+                                             __builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+  };
+  const auto xr = mk(X + (int64_t)m0 * ldx_b + koff, (int)(min(m_valid, 256) * ldx_b - koff));
+  const auto wr = mk(W + (int64_t)n0 * ldw_b + koff, (int)(min(n_valid, 256) * ldw_b - koff));
+  uint32_t xo[PPO], wo[PPO];
+#pragma unroll
+  for (int i = 0; i < PPO; ++i) {
+    const int r = (wave + i * NWAVE) * 8 + (lane >> 3);
+    const int c = swz_chunk(r, lane & 7);
+    xo[i] = (uint32_t)(min(r, m_valid - 1) * ldx_b) + (c << 4);
+    wo[i] = (uint32_t)(min(r, n_valid - 1) * ldw_b) + (c << 4);
+  }
+  auto xslot = [&](int kt) { return smem + (kt & 1) * 2 * kPPTile; };
+  auto wslot = [&](int kt) { return smem + (kt & 1) * 2 * kPPTile + kPPTile; };
+  g4_t g[2 * PPO];
+  auto gload = [&](int kt, int p) {
+    if constexpr (QIE_W4_ABL & 4) kt = 0;  // timing ablation: every load re-reads tile 0 (L2-resident)
+    if (p < PPO) g[p] = __builtin_amdgcn_raw_buffer_load_b128(xr, xo[p], kt * kRowBytes, 0);
+    else g[p] = __builtin_amdgcn_raw_buffer_load_b128(wr, wo[p - PPO], kt * kRowBytes, 0);
+  };
+  auto gstore = [&](int kt, int p) {
+    char QIE_LDS* dst = (p < PPO ? xslot(kt) + (wave + p * NWAVE) * 1024
+                                 : wslot(kt) + (wave + (p - PPO) * NWAVE) * 1024) + lane * 16;
+    *(g4_t QIE_LDS*)dst = g[p];
+  };
+
+  const int fr = lane & 15;
+  const int sw = (fr >> 1) & 7;
+  const int a_row = wm * 128 + fr, w_row = wn * 128 + fr;
+  auto ldfrag = [&](int kt, int ks, int r) -> frag {
+    const int cofs = ((4 * ks + (lane >> 4)) ^ sw) << 4;
+    if (r < 8) return *(const frag QIE_LDS*)(wslot(kt) + (w_row + 16 * r) * kRowBytes + cofs);
+    return *(const frag QIE_LDS*)(xslot(kt) + (a_row + 16 * (r - 8)) * kRowBytes + cofs);
+  };
+
+  accT acc[8][8];
+  frag wf[2][8], af[2][8];
+  // one k-step on set CUR; RD: read (rkt, rks) into CUR ^ 1; ST: write tile skt from g;
+  // LD: load tile lkt into g (after the stores that consumed it)
+  auto kstep = [&](auto cur_t, auto init_t, auto rd_t, auto st_t, auto ld_t, int rkt, int rks, int skt, int lkt) {
+    constexpr int CUR = decltype(cur_t)::value;
+    constexpr bool INIT = decltype(init_t)::value, RD = decltype(rd_t)::value;
+    constexpr bool ST = decltype(st_t)::value, LD = decltype(ld_t)::value;
+#pragma unroll
+    for (int q = 0; q < 64; ++q) {
+      const int i = q >> 3, j = q & 7;
+      if constexpr (INIT) Mma4<I8>::init(acc[i][j], wf[CUR][j], af[CUR][i]);
+      else Mma4<I8>::acc(acc[i][j], wf[CUR][j], af[CUR][i]);
+      if constexpr (RD) {
+        if ((q & 3) == 1) {
+          const int r = q >> 2;
+          if (r < 8) wf[CUR ^ 1][r] = ldfrag(rkt, rks, r);
+          else af[CUR ^ 1][r - 8] = ldfrag(rkt, rks, r);
+        }
+      }
+      if constexpr (ST) {
+        if ((q & 3) == 2) gstore(skt, q >> 2);
+      }
+      if constexpr (LD) {
+        if ((q & 3) == 3) gload(lkt, q >> 2);
+      }
+    }
+  };
+  using T = std::true_type;
+  using F = std::false_type;
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  // this wave's LDS stores / reads retired, then the barrier: no vmcnt, so the register loads of
+  // tile k+3 stay in flight across it (hipcc's own counted waits guard their use in the stores)
+  auto bar = [&]() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+
+  // prologue: tiles 0 and 1 into LDS, tile 2 into registers, tile 0's k-step 0 fragments read
+#pragma unroll
+  for (int p = 0; p < 2 * PPO; ++p) gload(0, p);
+#pragma unroll
+  for (int p = 0; p < 2 * PPO; ++p) gstore(0, p);
+#pragma unroll
+  for (int p = 0; p < 2 * PPO; ++p) gload(1, p);
+#pragma unroll
+  for (int p = 0; p < 2 * PPO; ++p) gstore(1, p);
+#pragma unroll
+  for (int p = 0; p < 2 * PPO; ++p) gload(2, p);
+  bar();
+#pragma unroll
+  for (int r = 0; r < 8; ++r) wf[0][r] = ldfrag(0, 0, r);
+#pragma unroll
+  for (int r = 0; r < 8; ++r) af[0][r] = ldfrag(0, 0, 8 + r);
+
+  // tile kt: stage A, barrier, stage B (reads tile kt+1, stores tile kt+2, loads tile kt+3)
+  int kt = 0;
+  kstep(I0{}, T{}, T{}, F{}, F{}, 0, 1, 0, 0);
+  bar();
+  if (nk > 3) {
+    kstep(I1{}, F{}, T{}, T{}, T{}, 1, 0, 2, 3);
+    for (kt = 1; kt < nk - 3; ++kt) {
+      kstep(I0{}, F{}, T{}, F{}, F{}, kt, 1, 0, 0);
+      bar();
+      kstep(I1{}, F{}, T{}, T{}, T{}, kt + 1, 0, kt + 2, kt + 3);
+    }
+    kstep(I0{}, F{}, T{}, F{}, F{}, kt, 1, 0, 0);  // nk-3
+    bar();
+  }
+  kstep(I1{}, F{}, T{}, T{}, F{}, kt + 1, 0, kt + 2, 0);  // stores the last tile nk-1
+  ++kt;
+  kstep(I0{}, F{}, T{}, F{}, F{}, kt, 1, 0, 0);  // nk-2
+  bar();
+  kstep(I1{}, F{}, T{}, F{}, F{}, kt + 1, 0, 0, 0);
+  kstep(I0{}, F{}, T{}, F{}, F{}, kt + 1, 1, 0, 0);  // nk-1
+  kstep(I1{}, F{}, F{}, F{}, F{}, 0, 0, 0, 0);
+
+  ring_epilogue<8, EPI, I8>(acc, e, M, N, m0 + wm * 128, n0 + wn * 128, lane, smem);
+}
+
 template <int EPI, bool I8>
 int launch_gemm(const void* x, int64_t ldx, const void* w, int64_t ldw, int M, int N, int K,
                 const EpiArgs& e, hipStream_t s) {
@@ -1183,7 +1334,10 @@ int launch_gemm(const void* x, int64_t ldx, const void* w, int64_t ldw, int M, i
                     (EPI != EPI_GATE_RES || (((uintptr_t)e.gate % 16) == 0 && e.gate_bstride % 8 == 0)) &&
                     (EPI != EPI_QKV || e.head_dim % 8 == 0);
   if (wide && M >= 256 && N >= 256 && big_tiles >= 160 && kb >= (kRingD + 2) * k4RowBytes) {
-    if constexpr (QIE_GEMM_W4 && EPI != EPI_QKV_NR)
+    if constexpr (QIE_GEMM_W4 == 2 && EPI != EPI_QKV_NR)
+      gemm_w4s_kernel<EPI, I8><<<(int)big_tiles, 256, 0, s>>>((const char*)x, ldx_b, (const char*)w, ldw_b, M, N,
+                                                             kb, e);
+    else if constexpr (QIE_GEMM_W4 == 1 && EPI != EPI_QKV_NR)
       gemm_w4_kernel<EPI, I8><<<(int)big_tiles, 256, 0, s>>>((const char*)x, ldx_b, (const char*)w, ldw_b, M, N,
                                                             kb, e);
     else if constexpr (QIE_GEMM_PP)  // (kb % 128 == 0 and kb >= 320 hold, so nk >= 3)
