@@ -253,3 +253,52 @@ def test_encoder_linears_splitk():
     rd = r.to(DEV)
     lin.residual(x.to(DEV), w.to(DEV), b.to(DEV), torch.ones(1, N, dtype=BF16, device=DEV), rd)
     assert _rel(rd, r.float() + want) <= 4e-3
+
+
+def test_pipeline_prompt_hook_end_to_end():
+    """pipe(image=PIL, prompt=str) through QwenImageEditPromptEncoder (tiny Qwen2.5-VL on the HIP
+    path behind a stub processor) == pipe(prompt_embeds=hook(prompt, image)); the hook drops the
+    first 64 tokens of the encoder's hidden states."""
+    from PIL import Image
+    from oracle import dit_ref as R
+    from oracle import vl_ref as VL
+    from qwen_image_edit_streamdiffusion_amd import QwenImageEditPlusPipeline, QwenImageTransformer2DModel
+    from qwen_image_edit_streamdiffusion_amd.text_encoder import (QwenImageEditPromptEncoder, QwenVLEncoder,
+                                                                  TextEncoderConfig)
+    from qwen_image_edit_streamdiffusion_amd.vision import VisionConfig
+    from qwen_image_edit_streamdiffusion_amd.vae import QwenImageVAEDecoder, QwenImageVAEEncoder, VAEConfig
+    cfg = R.tiny_config()
+    _, sd = VL.tiny_vl_model(5, text_hidden=cfg.joint_attention_dim, text_heads=1)
+    enc = QwenVLEncoder(TextEncoderConfig(vocab_size=1000, hidden_size=cfg.joint_attention_dim, intermediate_size=512,
+                                          num_hidden_layers=2, num_attention_heads=1, num_key_value_heads=1),
+                        VisionConfig(depth=4, hidden_size=320, intermediate_size=200, num_heads=4,
+                                     out_hidden_size=cfg.joint_attention_dim, fullatt_block_indexes=(1, 3)),
+                        DEV, image_token_id=990).load_state_dict(sd)
+    g = torch.Generator().manual_seed(31)
+    ids = torch.cat([torch.randint(0, 900, (70,), generator=g), torch.tensor([992]), torch.full((16,), 990),
+                     torch.tensor([993]), torch.randint(0, 900, (12,), generator=g)])
+    pv = torch.randn(64, 1176, generator=g)
+    seen = []
+
+    class Proc:  # the processor's contract: input_ids, pixel_values, image_grid_thw
+        def __call__(self, text, images=None, return_tensors=None):
+            seen.append((text, images))
+            return {"input_ids": ids.view(1, -1), "attention_mask": torch.ones(1, ids.numel(), dtype=torch.long),
+                    "pixel_values": pv, "image_grid_thw": torch.tensor([[1, 8, 8]])}
+
+    hook = QwenImageEditPromptEncoder(enc, Proc())
+    e, msk = hook("make it red", Image.new("RGB", (640, 480)))
+    want = enc(ids, pv, torch.tensor([[1, 8, 8]]))[64:]
+    assert e.shape == (1, ids.numel() - 64, cfg.joint_attention_dim) and torch.equal(e[0], want)
+    assert seen[0][1][0].size == (448, 320)  # condition image resized to the 384^2 area
+    m = QwenImageTransformer2DModel(num_layers=cfg.num_layers, num_attention_heads=cfg.num_attention_heads,
+                                    joint_attention_dim=cfg.joint_attention_dim, device=DEV)
+    m.load_diffusers_state_dict(R.random_params(cfg, seed=0))
+    pipe = QwenImageEditPlusPipeline(m, prompt_encoder=hook)
+    pipe.vae = QwenImageVAEDecoder(VAEConfig(base_dim=16), DEV).random_init_(7)
+    pipe.vae_encoder = QwenImageVAEEncoder(VAEConfig(base_dim=16), DEV).random_init_(8)
+    im = Image.fromarray(torch.randint(0, 256, (256, 256, 3), generator=g, dtype=torch.uint8).numpy())
+    kw = dict(num_inference_steps=2, height=128, width=128, output_type="uint8")
+    a = pipe(image=im, prompt="make it red", generator=torch.Generator().manual_seed(42), **kw).images
+    b = pipe(image=im, prompt_embeds=e, prompt_embeds_mask=msk, generator=torch.Generator().manual_seed(42), **kw).images
+    assert a.shape == (1, 128, 128, 3) and torch.equal(a, b)

@@ -134,3 +134,31 @@ def test_load_prompt_encoder_from_snapshot(tmp_path):
     assert enc.vision.config.intermediate_size == 200 and enc.image_token_id == 990
     assert torch.equal(enc.text.w["embed"], sd["language_model.embed_tokens.weight"])
     assert torch.equal(enc.vision.blocks[1]["w_down"][:, :200], sd["visual.blocks.1.mlp.down_proj.weight"])
+
+
+def test_from_pretrained_wires_snapshot_prompt_encoder(tmp_path, monkeypatch):
+    """A snapshot with text_encoder/ + processor/ gives pipe.prompt_encoder (loaded on the CPU here;
+    the processor is stubbed -- the tokenizer files come with a real checkpoint)."""
+    import json
+    import transformers
+    from safetensors.torch import save_file
+    vl = pytest.importorskip("oracle.vl_ref")
+    from qwen_image_edit_streamdiffusion_amd.pipeline import QwenImageEditPlusPipeline
+    from qwen_image_edit_streamdiffusion_amd.text_encoder import QwenImageEditPromptEncoder
+    m, sd = vl.tiny_vl_model(6)
+    d = tmp_path / "text_encoder"
+    d.mkdir()
+    (tmp_path / "processor").mkdir()
+    save_file({"model." + k: v.contiguous() for k, v in sd.items()}, str(d / "model.safetensors"))
+    (d / "config.json").write_text(json.dumps(m.config.to_dict()))
+    seen = {}
+
+    def fake_from_pretrained(path, **kw):
+        seen["path"], seen["kw"] = path, kw
+        return "processor"
+
+    monkeypatch.setattr(transformers.AutoProcessor, "from_pretrained", staticmethod(fake_from_pretrained))
+    hook = QwenImageEditPlusPipeline._snapshot_prompt_encoder(str(tmp_path), "cpu")
+    assert isinstance(hook, QwenImageEditPromptEncoder) and hook.processor == "processor"
+    assert seen["path"].endswith("processor") and seen["kw"].get("local_files_only") is True
+    assert hook.encoder.text.config.hidden_size == 256 and hook.encoder.image_token_id == 990
