@@ -79,7 +79,7 @@ def images_to_rgb(image, device) -> torch.Tensor:
         return t.to(device).contiguous()
     ims = image if isinstance(image, (list, tuple)) else [image]
     if len(ims) != 1:
-        raise NotImplementedError("one condition image per prompt on the HIP encoder path")
+        raise ValueError("images_to_rgb takes one PIL image (the pipeline encodes a list image by image)")
     import numpy as np
     from PIL import Image
     im = ims[0].convert("RGB")
@@ -184,9 +184,19 @@ class QwenImageEditPlusPipeline:
             if self.image_encoder is not None:
                 image_latents = self.image_encoder(image)
             elif self.vae_encoder is not None:
-                rgb = images_to_rgb(image, self.transformer.device)
-                image_latents = self.vae_encoder.encode(rgb)
-                shape = (rgb.shape[1] // 16, rgb.shape[2] // 16)
+                # Edit-Plus takes up to several condition images ("Picture 1", "Picture 2", ...): each
+                # is resized to the VAE area of its own aspect ratio and encoded on its own; their
+                # packed latents follow each other in the sequence, one img_shapes entry apiece
+                ims = image if isinstance(image, (list, tuple)) else [image]
+                if isinstance(image, torch.Tensor):
+                    ims = [image]
+                lat, shape = [], []
+                for im in ims:
+                    rgb = images_to_rgb(im, self.transformer.device)
+                    lat.append(self.vae_encoder.encode(rgb))
+                    shape.append((rgb.shape[1] // 16, rgb.shape[2] // 16))
+                image_latents = lat[0] if len(lat) == 1 else torch.cat(lat, 1)
+                shape = shape[0] if len(shape) == 1 else shape
             else:
                 raise NotImplementedError(
                     "no VAE encoder: pass image_latents= (packed [B, S, 64]), set pipe.vae_encoder or "
@@ -216,7 +226,7 @@ class QwenImageEditPlusPipeline:
                  generator: Optional[torch.Generator] = None, latents: Optional[torch.Tensor] = None,
                  prompt_embeds=None, prompt_embeds_mask=None, negative_prompt_embeds=None,
                  negative_prompt_embeds_mask=None, image_latents=None,
-                 cond_shape: Optional[Tuple[int, int]] = None, output_type: str = "pil",
+                 cond_shape=None, output_type: str = "pil",
                  return_dict: bool = True, batched_cfg: bool = True, **unused):
         # guidance_scale is a no-op for this non-guidance-distilled model [U]
         dev = self.transformer.device
@@ -250,7 +260,10 @@ class QwenImageEditPlusPipeline:
         if cond_shape is None:
             side = int(round(math.sqrt(cond.shape[1])))
             cond_shape = (side, cond.shape[1] // side)
-        img_shapes = [[(1, lh, lw), (1, cond_shape[0], cond_shape[1])]] * B
+        cond_shapes = [tuple(cond_shape)] if isinstance(cond_shape[0], int) else [tuple(c) for c in cond_shape]
+        if sum(h * w for h, w in cond_shapes) != cond.shape[1]:
+            raise ValueError(f"cond_shape {cond_shapes} does not cover the {cond.shape[1]} condition tokens")
+        img_shapes = [[(1, lh, lw)] + [(1, h, w) for h, w in cond_shapes]] * B
 
         sch = self.scheduler
         c = sch.config

@@ -186,3 +186,45 @@ def test_int8_image_roundtrip_bitwise(dev, tiny, tmp_path):
     assert torch.equal(a, b)
     pipe = QwenImageEditPlusPipeline.from_pretrained(str(tmp_path), device=dev)
     assert pipe.transformer.int8_only
+
+
+def test_forward_three_image_segments_vs_oracle(dev, tiny):
+    """Edit-Plus with two condition images: img_shapes carries three (frame, h, w) entries, each a
+    RoPE frame index of its own (noise latents, picture 1, picture 2 of another size)."""
+    cfg, params, m = tiny
+    g = torch.Generator().manual_seed(41)
+    shapes = [(1, 8, 8), (1, 8, 8), (1, 4, 8)]
+    S = sum(f * h * w for f, h, w in shapes)
+    hs = torch.randn(1, S, 64, generator=g).to(torch.bfloat16)
+    enc = torch.randn(1, 12, cfg.joint_attention_dim, generator=g).to(torch.bfloat16)
+    t = R.model_timestep(torch.tensor([500.0]))
+    out = m(hs.to(dev), enc.to(dev), None, t.to(dev), [shapes], [12], return_dict=False)[0]
+    ref = R.transformer_forward(params, cfg, hs, enc, t, shapes, [12])
+    assert ((out.float().cpu() - ref).norm() / ref.norm()).item() <= 2e-2
+
+
+def test_pipeline_two_condition_images(dev, tiny):
+    """pipe(image=[PIL, PIL]) VAE-encodes each picture at its own aspect ratio and concatenates
+    them == pipe(image_latents=cat(...), cond_shape=[...])."""
+    from PIL import Image
+    from qwen_image_edit_streamdiffusion_amd import QwenImageEditPlusPipeline
+    from qwen_image_edit_streamdiffusion_amd.pipeline import images_to_rgb
+    from qwen_image_edit_streamdiffusion_amd.vae import QwenImageVAEDecoder, QwenImageVAEEncoder, VAEConfig
+    cfg, params, m = tiny
+    pipe = QwenImageEditPlusPipeline(m)
+    pipe.vae = QwenImageVAEDecoder(VAEConfig(base_dim=16), dev).random_init_(7)
+    pipe.vae_encoder = QwenImageVAEEncoder(VAEConfig(base_dim=16), dev).random_init_(8)
+    g = torch.Generator().manual_seed(43)
+    ims = [Image.fromarray(torch.randint(0, 256, (h, w, 3), generator=g, dtype=torch.uint8).numpy())
+           for h, w in ((300, 300), (200, 400))]
+    pe = torch.randn(1, 20, cfg.joint_attention_dim, generator=g).to(torch.bfloat16).to(dev)
+    kw = dict(prompt_embeds=pe, num_inference_steps=2, height=128, width=128, output_type="uint8")
+    a = pipe(image=ims, generator=torch.Generator().manual_seed(42), **kw).images
+    rgbs = [images_to_rgb(im, dev) for im in ims]
+    assert rgbs[0].shape[1:3] == (1024, 1024) and rgbs[1].shape[1] < rgbs[1].shape[2]  # own aspect ratios
+    lat = torch.cat([pipe.vae_encoder.encode(r) for r in rgbs], 1)
+    shapes = [(r.shape[1] // 16, r.shape[2] // 16) for r in rgbs]
+    b = pipe(image_latents=lat, cond_shape=shapes, generator=torch.Generator().manual_seed(42), **kw).images
+    assert a.shape == (1, 128, 128, 3) and torch.equal(a, b)
+    with pytest.raises(ValueError):
+        pipe(image_latents=lat, cond_shape=shapes[:1], generator=torch.Generator().manual_seed(42), **kw)
