@@ -1242,10 +1242,14 @@ __global__ void __launch_bounds__(256, 1)
 
   accT acc[8][8];
   frag wf[2][8], af[2][8];
-  // one k-step on set CUR; RD: read (rkt, rks) into CUR ^ 1; ST: write tile skt from g;
-  // LD: load tile lkt into g (after the stores that consumed it)
+  // one k-step on set CUR; RD: read (rkt, rks) into CUR ^ 1; ST: write half H (8 pieces) of tile
+  // skt from g; LD: then reload that half of g with tile lkt. Stage A (CUR 0) moves half 1, stage
+  // B (CUR 1) half 0, so each stage carries 16 fragment reads and 8 tile stores: tile j's half 0
+  // is stored in stage B of tile j-2, its half 1 in stage A of tile j-1 (slot j & 1 is free from
+  // the barrier of tile j-2 on), and both are visible after the barrier of tile j-1.
   auto kstep = [&](auto cur_t, auto init_t, auto rd_t, auto st_t, auto ld_t, int rkt, int rks, int skt, int lkt) {
     constexpr int CUR = decltype(cur_t)::value;
+    constexpr int H = CUR ^ 1;
     constexpr bool INIT = decltype(init_t)::value, RD = decltype(rd_t)::value;
     constexpr bool ST = decltype(st_t)::value, LD = decltype(ld_t)::value;
 #pragma unroll
@@ -1261,10 +1265,10 @@ __global__ void __launch_bounds__(256, 1)
         }
       }
       if constexpr (ST) {
-        if ((q & 3) == 2) gstore(skt, q >> 2);
+        if ((q & 7) == 3) gstore(skt, 8 * H + (q >> 3));
       }
       if constexpr (LD) {
-        if ((q & 3) == 3) gload(lkt, q >> 2);
+        if ((q & 7) == 7) gload(lkt, 8 * H + (q >> 3));
       }
     }
   };
@@ -1272,11 +1276,11 @@ __global__ void __launch_bounds__(256, 1)
   using F = std::false_type;
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
-  // this wave's LDS stores / reads retired, then the barrier: no vmcnt, so the register loads of
-  // tile k+3 stay in flight across it (hipcc's own counted waits guard their use in the stores)
+  // this wave's LDS stores / reads retired, then the barrier: no vmcnt, so the register loads
+  // stay in flight across it (hipcc's own counted waits guard their use in the stores)
   auto bar = [&]() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
 
-  // prologue: tiles 0 and 1 into LDS, tile 2 into registers, tile 0's k-step 0 fragments read
+  // prologue: tile 0 and half 0 of tile 1 into LDS; g = [tile 2 half 0 | tile 1 half 1]
 #pragma unroll
   for (int p = 0; p < 2 * PPO; ++p) gload(0, p);
 #pragma unroll
@@ -1284,35 +1288,39 @@ __global__ void __launch_bounds__(256, 1)
 #pragma unroll
   for (int p = 0; p < 2 * PPO; ++p) gload(1, p);
 #pragma unroll
-  for (int p = 0; p < 2 * PPO; ++p) gstore(1, p);
+  for (int p = 0; p < PPO; ++p) gstore(1, p);
 #pragma unroll
-  for (int p = 0; p < 2 * PPO; ++p) gload(2, p);
+  for (int p = 0; p < PPO; ++p) gload(2, p);
   bar();
 #pragma unroll
   for (int r = 0; r < 8; ++r) wf[0][r] = ldfrag(0, 0, r);
 #pragma unroll
   for (int r = 0; r < 8; ++r) af[0][r] = ldfrag(0, 0, 8 + r);
 
-  // tile kt: stage A, barrier, stage B (reads tile kt+1, stores tile kt+2, loads tile kt+3)
+  // tile kt: A = k-step 0, stores tile kt+1 half 1, loads tile kt+2 half 1; barrier;
+  //          B = k-step 1, reads tile kt+1 k-step 0, stores tile kt+2 half 0, loads tile kt+3 half 0
   int kt = 0;
-  kstep(I0{}, T{}, T{}, F{}, F{}, 0, 1, 0, 0);
-  bar();
   if (nk > 3) {
+    kstep(I0{}, T{}, T{}, T{}, T{}, 0, 1, 1, 2);
+    bar();
     kstep(I1{}, F{}, T{}, T{}, T{}, 1, 0, 2, 3);
     for (kt = 1; kt < nk - 3; ++kt) {
-      kstep(I0{}, F{}, T{}, F{}, F{}, kt, 1, 0, 0);
+      kstep(I0{}, F{}, T{}, T{}, T{}, kt, 1, kt + 1, kt + 2);
       bar();
       kstep(I1{}, F{}, T{}, T{}, T{}, kt + 1, 0, kt + 2, kt + 3);
     }
-    kstep(I0{}, F{}, T{}, F{}, F{}, kt, 1, 0, 0);  // nk-3
-    bar();
+    kstep(I0{}, F{}, T{}, T{}, T{}, kt, 1, kt + 1, kt + 2);  // nk-3
+  } else {
+    kstep(I0{}, T{}, T{}, T{}, T{}, 0, 1, 1, 2);  // nk == 3: tile 0 is nk-3
   }
-  kstep(I1{}, F{}, T{}, T{}, F{}, kt + 1, 0, kt + 2, 0);  // stores the last tile nk-1
-  ++kt;
-  kstep(I0{}, F{}, T{}, F{}, F{}, kt, 1, 0, 0);  // nk-2
+  bar();
+  kstep(I1{}, F{}, T{}, T{}, F{}, kt + 1, 0, kt + 2, 0);
+  ++kt;  // nk-2
+  kstep(I0{}, F{}, T{}, T{}, F{}, kt, 1, kt + 1, 0);
   bar();
   kstep(I1{}, F{}, T{}, F{}, F{}, kt + 1, 0, 0, 0);
-  kstep(I0{}, F{}, T{}, F{}, F{}, kt + 1, 1, 0, 0);  // nk-1
+  ++kt;  // nk-1
+  kstep(I0{}, F{}, T{}, F{}, F{}, kt, 1, 0, 0);
   kstep(I1{}, F{}, F{}, F{}, F{}, 0, 0, 0, 0);
 
   ring_epilogue<8, EPI, I8>(acc, e, M, N, m0 + wm * 128, n0 + wn * 128, lane, smem);
