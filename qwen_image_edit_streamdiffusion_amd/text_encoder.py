@@ -18,7 +18,9 @@ lengths are a few hundred tokens, so the full score blocks stay small).
 """
 from __future__ import annotations
 
+import hashlib
 import math
+from collections import OrderedDict
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Tuple
 
@@ -296,7 +298,7 @@ class QwenVLEncoder:
     IMAGE_TOKEN_ID = 151655  # <|image_pad|> in the Qwen2.5-VL vocabulary
 
     def __init__(self, text_config: Optional[TextEncoderConfig] = None, vision_config=None, device="cuda",
-                 image_token_id: int = IMAGE_TOKEN_ID):
+                 image_token_id: int = IMAGE_TOKEN_ID, vision_cache_size: int = 8):
         from .vision import QwenVLVisionTower, VisionConfig
         self.text = QwenVLTextModel(text_config, device)
         self.vision = QwenVLVisionTower(vision_config or VisionConfig(), device)
@@ -304,6 +306,11 @@ class QwenVLEncoder:
             raise ValueError("vision out_hidden_size must equal the text hidden_size")
         self.image_token_id = image_token_id
         self.device = self.text.device
+        # VLM cache (README.md:125,156,182 of the reference: cached_pipeline_v2 / test_vlm_cache):
+        # the vision tower's output per condition image, so a prompt change over the same image
+        # (the realtime loop's case) re-runs only the language model
+        self.vision_cache: "OrderedDict[tuple, torch.Tensor]" = OrderedDict()
+        self.vision_cache_size = vision_cache_size
 
     def load_state_dict(self, sd: Dict[str, torch.Tensor]) -> "QwenVLEncoder":
         self.text.load_state_dict({k: v for k, v in sd.items() if "visual." not in k})
@@ -322,7 +329,7 @@ class QwenVLEncoder:
         ids_dev[:S] = ids.to(dev).to(torch.int32)
         ops.embed_rows(self.text.w["embed"], ids_dev, out=emb)
         if pixel_values is not None:
-            img = self.vision(pixel_values, image_grid_thw)
+            img = self._vision(pixel_values, image_grid_thw)
             where = (ids.cpu() == self.image_token_id).nonzero().view(-1)
             if where.numel() != img.shape[0]:
                 raise ValueError(f"{where.numel()} image tokens but {img.shape[0]} image embeddings")
@@ -332,6 +339,32 @@ class QwenVLEncoder:
         return self.text(inputs_embeds=emb[:S], position_ids=pos)
 
     __call__ = forward
+
+    def _vision(self, pixel_values: torch.Tensor, image_grid_thw) -> torch.Tensor:
+        grid = tuple(tuple(int(v) for v in g) for g in (image_grid_thw.tolist() if torch.is_tensor(image_grid_thw)
+                                                         else image_grid_thw))
+        if self.vision_cache_size <= 0:
+            return self.vision.forward(pixel_values, grid)
+        pv = pixel_values.detach().to("cpu", torch.float32).contiguous()
+        key = (grid, hashlib.blake2b(pv.numpy().tobytes(), digest_size=16).hexdigest())
+        hit = self.vision_cache.get(key)
+        if hit is not None:
+            self.vision_cache.move_to_end(key)
+            return hit
+        img = self.vision.forward(pixel_values, grid)
+        self.vision_cache[key] = img
+        while len(self.vision_cache) > self.vision_cache_size:
+            self.vision_cache.popitem(last=False)
+        return img
+
+
+def _image_digest(im) -> str:
+    """Content key of a condition image (PIL or tensor) for the prompt-embedding cache."""
+    if torch.is_tensor(im):
+        data, tag = im.detach().cpu().contiguous().numpy().tobytes(), (tuple(im.shape), str(im.dtype))
+    else:
+        data, tag = im.tobytes(), (im.size, im.mode)
+    return hashlib.blake2b(repr(tag).encode() + data, digest_size=16).hexdigest()
 
 
 # ---------------------------------------------------------------------------- pipeline hook
@@ -361,8 +394,13 @@ class QwenImageEditPromptEncoder:
     ``processor(text=[str], images=[PIL...], return_tensors="pt")`` must return input_ids,
     pixel_values and image_grid_thw (the HF processor's keys)."""
 
-    def __init__(self, encoder: QwenVLEncoder, processor, drop_tokens: int = PROMPT_DROP_TOKENS):
+    def __init__(self, encoder: QwenVLEncoder, processor, drop_tokens: int = PROMPT_DROP_TOKENS,
+                 cache_size: int = 32):
         self.encoder, self.processor, self.drop = encoder, processor, drop_tokens
+        # prompt-embedding cache keyed by (prompt, condition-image contents): the reference's
+        # cached_pipeline (README.md:124) reuse of prompt / image embeddings
+        self.cache: "OrderedDict[tuple, tuple]" = OrderedDict()
+        self.cache_size = cache_size
 
     def _condition_images(self, image):
         if image is None:
@@ -379,6 +417,19 @@ class QwenImageEditPromptEncoder:
 
     def __call__(self, prompt, image=None):
         prompts = [prompt] if isinstance(prompt, str) else list(prompt)
+        ims = [] if image is None else (image if isinstance(image, (list, tuple)) else [image])
+        key = (tuple(prompts), tuple(_image_digest(im) for im in ims)) if self.cache_size > 0 else None
+        if key is not None and key in self.cache:
+            self.cache.move_to_end(key)
+            return self.cache[key]
+        out = self._encode(prompts, image)
+        if key is not None:
+            self.cache[key] = out
+            while len(self.cache) > self.cache_size:
+                self.cache.popitem(last=False)
+        return out
+
+    def _encode(self, prompts, image):
         imgs = self._condition_images(image)
         prefix = "".join(IMAGE_PROMPT_TEMPLATE.format(i + 1) for i in range(len(imgs)))
         rows = []

@@ -302,3 +302,26 @@ def test_pipeline_prompt_hook_end_to_end():
     a = pipe(image=im, prompt="make it red", generator=torch.Generator().manual_seed(42), **kw).images
     b = pipe(image=im, prompt_embeds=e, prompt_embeds_mask=msk, generator=torch.Generator().manual_seed(42), **kw).images
     assert a.shape == (1, 128, 128, 3) and torch.equal(a, b)
+
+
+def test_vl_encoder_vision_cache():
+    """Same condition image, new prompt: the vision tower runs once (VLM cache) and the result
+    equals the uncached encoder's."""
+    from oracle import vl_ref as VL
+    from qwen_image_edit_streamdiffusion_amd.text_encoder import QwenVLEncoder, TextEncoderConfig
+    _, sd = VL.tiny_vl_model(2)
+    tc = TextEncoderConfig(vocab_size=1000, hidden_size=256, intermediate_size=512, num_hidden_layers=2,
+                           num_attention_heads=2, num_key_value_heads=1)
+    enc = QwenVLEncoder(tc, _vision_cfg(), DEV, image_token_id=990).load_state_dict(sd)
+    ref = QwenVLEncoder(tc, _vision_cfg(), DEV, image_token_id=990, vision_cache_size=0).load_state_dict(sd)
+    runs = []
+    tower = enc.vision.forward
+    enc.vision.forward = lambda *a, **k: runs.append(1) or tower(*a, **k)
+    g = torch.Generator().manual_seed(12)
+    grid = torch.tensor([[1, 8, 8]])
+    pv = torch.randn(64, 1176, generator=g)
+    for n in (30, 41):
+        ids = torch.cat([torch.randint(0, 900, (n,), generator=g), torch.full((16,), 990), torch.arange(5)])
+        got = enc(ids, pv, grid)
+        assert torch.equal(got, ref(ids, pv, grid))
+    assert len(enc.vision_cache) == 1 and len(runs) == 1

@@ -162,3 +162,31 @@ def test_from_pretrained_wires_snapshot_prompt_encoder(tmp_path, monkeypatch):
     assert isinstance(hook, QwenImageEditPromptEncoder) and hook.processor == "processor"
     assert seen["path"].endswith("processor") and seen["kw"].get("local_files_only") is True
     assert hook.encoder.text.config.hidden_size == 256 and hook.encoder.image_token_id == 990
+
+
+def test_prompt_hook_cache():
+    """Repeated (prompt, image) pairs are served from the embedding cache; a new prompt or new
+    image contents miss it; the LRU bound holds."""
+    from PIL import Image
+    from qwen_image_edit_streamdiffusion_amd.text_encoder import QwenImageEditPromptEncoder
+    calls = []
+
+    class Proc:
+        def __call__(self, text, images=None, return_tensors=None):
+            calls.append(text[0])
+            return {"input_ids": torch.arange(70).view(1, -1)}
+
+    class Enc:
+        def __call__(self, ids, pv, grid):
+            return torch.full((ids.numel(), 4), float(len(calls)), dtype=torch.bfloat16)
+
+    hook = QwenImageEditPromptEncoder(Enc(), Proc(), cache_size=2)
+    a, b = Image.new("RGB", (64, 64), "red"), Image.new("RGB", (64, 64), "blue")
+    e1, _ = hook("x", a)
+    e2, _ = hook("x", Image.new("RGB", (64, 64), "red"))  # same contents, new object
+    assert len(calls) == 1 and e2 is e1
+    hook("x", b)
+    hook("y", a)
+    assert len(calls) == 3
+    hook("x", a)  # evicted by the bound of 2
+    assert len(calls) == 4
