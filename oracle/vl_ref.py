@@ -7,7 +7,6 @@ weights exist offline, so parity is on random weights of reduced width (the same
 7B checkpoint runs)."""
 from __future__ import annotations
 
-from typing import Dict, Tuple
 
 import torch
 

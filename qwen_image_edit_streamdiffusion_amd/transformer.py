@@ -21,8 +21,7 @@ HBM layout per forward (B rows, S_img image tokens, S_txt text tokens):
 from __future__ import annotations
 
 import contextlib
-import math
-from dataclasses import asdict, dataclass, field
+from dataclasses import dataclass
 from typing import Dict, Iterator, List, Optional, Sequence, Tuple
 
 import torch

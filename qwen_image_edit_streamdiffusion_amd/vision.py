@@ -19,7 +19,6 @@ window permutation and its inverse are row gathers (the embedding kernel).
 """
 from __future__ import annotations
 
-import math
 from dataclasses import dataclass
 from typing import Dict, List, Sequence, Tuple
 

@@ -13,7 +13,7 @@ from __future__ import annotations
 import glob
 import os
 import re
-from typing import Dict, Iterable, Optional, Tuple
+from typing import Dict, Iterable, Optional
 
 import torch
 
