@@ -72,15 +72,16 @@ def rotary_reference(hidden: int, heads: int, mrope, position_ids: torch.Tensor,
 
 def tiny_vl_model(seed: int = 0, text_hidden: int = 256, vis_hidden: int = 320, vis_heads: int = 4,
                   vis_intermediate: int = 200, depth: int = 4, fullatt=(1, 3), image_token_id: int = 990,
-                  text_heads: int = 2):
+                  text_heads: int = 2, text_kv_heads: int = 1, text_layers: int = 2, text_intermediate: int = 512):
     """A random transformers Qwen2_5_VLModel (vision tower + language model, fp32 eager) whose
     weights are bf16-representable, and its state_dict. The vision head_dim is 80 (as in the 7B
     checkpoint) and the MLP width 200 is not a multiple of 64 (the HIP path pads both)."""
     from transformers import Qwen2_5_VLConfig
     from transformers.models.qwen2_5_vl.modeling_qwen2_5_vl import Qwen2_5_VLModel
     cfg = Qwen2_5_VLConfig(
-        text_config=dict(vocab_size=1000, hidden_size=text_hidden, bos_token_id=0, eos_token_id=1, intermediate_size=512, num_hidden_layers=2,
-                         num_attention_heads=text_heads, num_key_value_heads=1, rms_norm_eps=1e-6,
+        text_config=dict(vocab_size=1000, hidden_size=text_hidden, bos_token_id=0, eos_token_id=1,
+                         intermediate_size=text_intermediate, num_hidden_layers=text_layers,
+                         num_attention_heads=text_heads, num_key_value_heads=text_kv_heads, rms_norm_eps=1e-6,
                          rope_parameters={"rope_type": "default", "rope_theta": 1e6, "mrope_section": [16, 24, 24]}),
         vision_config=dict(depth=depth, hidden_size=vis_hidden, intermediate_size=vis_intermediate,
                            num_heads=vis_heads, out_hidden_size=text_hidden, fullatt_block_indexes=list(fullatt),

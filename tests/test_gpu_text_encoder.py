@@ -325,3 +325,27 @@ def test_vl_encoder_vision_cache():
         got = enc(ids, pv, grid)
         assert torch.equal(got, ref(ids, pv, grid))
     assert len(enc.vision_cache) == 1 and len(runs) == 1
+
+
+def test_vl_encoder_full_width_one_layer():
+    """Qwen2.5-VL-7B widths (text 3584 / 28 heads / 4 kv heads / SwiGLU 18944; vision 1280 / 16 heads
+    of 80 / SwiGLU 3420 / merger 5120 -> 3584) with one text layer and two vision blocks (one window,
+    one full), on a 392^2 condition image (28 x 28 patches) inside a 300-token prompt: the real GQA
+    group of 7, the real head-slot padding and the real window raggedness vs transformers."""
+    from oracle import vl_ref as VL
+    from qwen_image_edit_streamdiffusion_amd.text_encoder import QwenVLEncoder, TextEncoderConfig
+    from qwen_image_edit_streamdiffusion_amd.vision import VisionConfig
+    m, sd = VL.tiny_vl_model(9, text_hidden=3584, vis_hidden=1280, vis_heads=16, vis_intermediate=3420, depth=2,
+                             fullatt=(1,), text_heads=28, text_kv_heads=4, text_layers=1, text_intermediate=18944)
+    enc = QwenVLEncoder(TextEncoderConfig(vocab_size=1000, hidden_size=3584, intermediate_size=18944,
+                                          num_hidden_layers=1, num_attention_heads=28, num_key_value_heads=4),
+                        VisionConfig(depth=2, fullatt_block_indexes=(1,)), DEV, image_token_id=990).load_state_dict(sd)
+    g = torch.Generator().manual_seed(13)
+    grid = torch.tensor([[1, 28, 28]])
+    pv = torch.randn(784, 1176, generator=g)
+    ids = torch.cat([torch.randint(0, 900, (70,), generator=g), torch.tensor([992]), torch.full((196,), 990),
+                     torch.tensor([993]), torch.randint(0, 900, (32,), generator=g)])
+    want, _ = VL.vl_forward(m, ids, pv, grid)
+    got = enc(ids, pv, grid)
+    assert got.shape == want.shape == (300, 3584)
+    assert _rel(got, want) <= 2e-2
