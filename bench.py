@@ -140,6 +140,8 @@ def main():
                          "latency-oriented split rule ops.splitk_splits)")
     ap.add_argument("--no-text-overlap", action="store_true",
                     help="A/B: run the text stream on the caller's stream, not on a second HIP stream")
+    ap.add_argument("--no-batched-mod", action="store_true",
+                    help="A/B: one modulation GEMV launch per block and stream, not one for all blocks")
     ap.add_argument("--force-dist", action="store_true",
                     help="debug: run the collective path (process group, broadcast, gather, "
                          "barriers, max-reduce) even at world size 1")
@@ -168,6 +170,7 @@ def main():
     model.overlap_text_stream = not args.no_text_overlap
     model.fuse_qk_norm_rope = not args.no_qk_fusion
     model.log2q_attention = not args.no_log2q
+    model.batched_modulation = not args.no_batched_mod
     model.text_splits = args.text_splits or None
     decode = args.vae in ("both", "decode")
     encode = args.vae == "both"

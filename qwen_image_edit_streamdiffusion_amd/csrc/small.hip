@@ -105,8 +105,18 @@ __global__ void pack_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y
 }
 
 // Skinny GEMV: y[m][n] = bf16(sum_k x[m][k] w[n][k] + bias[n]) for m < M <= MM.
-// One wave computes 4 output columns; lanes stride K in 16-byte chunks.
-template <int MM>
+// One wave computes 4 output columns; lanes stride K in 16-byte chunks. HBM-bound on W (the
+// modulation matrices are 113 MB each): every lane issues all U x 4 of a K-slab's W loads before
+// the first FMA, so a wave keeps U x 4 x 1 KB in flight instead of one row's 1 KB at a time
+// (U = 1 measured best: 22.5 us vs 24.1 us for the one-load-per-row form, HBM-cold 113 MB; U = 3 and 6
+// lose occupancy: 27 / 26 us).
+#ifndef QIE_GEMV_U
+#define QIE_GEMV_U 1
+#endif
+#ifndef QIE_GEMV_NT
+#define QIE_GEMV_NT 1
+#endif
+template <int MM, int U = QIE_GEMV_U>
 __global__ void __launch_bounds__(256)
     gemv_kernel(const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __restrict__ w,
                 const bf16_t* __restrict__ bias, bf16_t* __restrict__ y, int64_t ldy, int M, int N,
@@ -120,31 +130,44 @@ __global__ void __launch_bounds__(256)
   for (int m = 0; m < MM; ++m)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[m][j] = 0.f;
-  for (int c = lane; c < nch; c += 64) {
-    float wf[4][8];
+  const bf16_t* wrow[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int n = min(n0 + j, N - 1);
-      const u32x4_t ww = *(const u32x4_t*)(w + (int64_t)n * K + c * 8);
-      wf[j][0] = lo_f(ww.x); wf[j][1] = hi_f(ww.x); wf[j][2] = lo_f(ww.y); wf[j][3] = hi_f(ww.y);
-      wf[j][4] = lo_f(ww.z); wf[j][5] = hi_f(ww.z); wf[j][6] = lo_f(ww.w); wf[j][7] = hi_f(ww.w);
+  for (int j = 0; j < 4; ++j) wrow[j] = w + (int64_t)min(n0 + j, N - 1) * K;
+  for (int c0 = lane; c0 < nch; c0 += 64 * U) {
+    u32x4_t ww[U][4];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int c = min(c0 + u * 64, nch - 1);  // clamped reload of a valid chunk; its FMAs are skipped
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const u32x4_t* p = (const u32x4_t*)(wrow[j] + c * 8);
+        ww[u][j] = QIE_GEMV_NT ? __builtin_nontemporal_load(p) : *p;
+      }
     }
 #pragma unroll
-    for (int m = 0; m < MM; ++m) {
-      if (m < M) {
-        const u32x4_t xx = *(const u32x4_t*)(x + (int64_t)m * ldx + c * 8);
-        const float xf[8] = {lo_f(xx.x), hi_f(xx.x), lo_f(xx.y), hi_f(xx.y),
-                             lo_f(xx.z), hi_f(xx.z), lo_f(xx.w), hi_f(xx.w)};
+    for (int u = 0; u < U; ++u) {
+      const int c = c0 + u * 64;
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+      for (int m = 0; m < MM; ++m) {
+        if (m < M && c < nch) {
+          const u32x4_t xx = *(const u32x4_t*)(x + (int64_t)m * ldx + c * 8);
+          const float xf[8] = {lo_f(xx.x), hi_f(xx.x), lo_f(xx.y), hi_f(xx.y),
+                               lo_f(xx.z), hi_f(xx.z), lo_f(xx.w), hi_f(xx.w)};
 #pragma unroll
-          for (int e = 0; e < 8; ++e) acc[m][j] = __builtin_fmaf(xf[e], wf[j][e], acc[m][j]);
+          for (int j = 0; j < 4; ++j) {
+            const u32x4_t& q = ww[u][j];
+            const float wf[8] = {lo_f(q.x), hi_f(q.x), lo_f(q.y), hi_f(q.y),
+                                 lo_f(q.z), hi_f(q.z), lo_f(q.w), hi_f(q.w)};
+#pragma unroll
+            for (int e = 0; e < 8; ++e) acc[m][j] = __builtin_fmaf(xf[e], wf[e], acc[m][j]);
+          }
+        }
       }
     }
   }
 #pragma unroll
   for (int m = 0; m < MM; ++m) {
-    if (m >= M) break;
+    if (m >= M) continue;
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[m][j] = wave_sum(acc[m][j]);
     if (lane == 0) {

@@ -71,8 +71,10 @@ def gemv(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, out: Optional[torch.
     M, K = x.shape
     N = w.shape[0]
     _chk(M <= 16 and w.shape[1] == K and K % 8 == 0 and _is2d_rowmajor(x), "gemv shapes")
+    _chk(w.is_contiguous() and b.numel() == N, "gemv weight [N, K] contiguous, bias [N]")
     if out is None:
         out = torch.empty(M, N, dtype=BF16, device=x.device)
+    _chk(tuple(out.shape) == (M, N) and out.stride(1) == 1, "gemv out [M, N] (row stride any)")
     _lib.call("qie_gemv_bf16", _p(x), x.stride(0), _p(w), _p(b), _p(out), out.stride(0), M, N, K,
               _stream())
     return out

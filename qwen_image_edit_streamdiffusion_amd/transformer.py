@@ -66,16 +66,24 @@ class Transformer2DModelOutput:
 class _Block(nn.Module):
     """Packed weights of one QwenImageTransformerBlock."""
 
-    def __init__(self, D: int, Dh: int, F: int, device, dtype=BF16, int8_only: bool = False):
+    def __init__(self, D: int, Dh: int, F: int, device, dtype=BF16, int8_only: bool = False,
+                 mod_w: Optional[torch.Tensor] = None, mod_b: Optional[torch.Tensor] = None,
+                 mod_off: int = 0):
+        """``mod_w`` / ``mod_b``: the model's packed modulation weights [L * 2 * 6D, D] / [L * 2 * 6D];
+        this block's img_mod / txt_mod rows start at ``mod_off`` / ``mod_off + 6D``."""
         super().__init__()
         e = dict(device=device, dtype=dtype)
 
         def lin(*shape):  # bf16 weight of a quantised linear: absent when loaded pre-quantised
             return torch.empty(0, **e) if int8_only else torch.empty(*shape, **e)
 
-        for s in ("img", "txt"):
-            self.register_buffer(f"w_mod_{s}", torch.empty(6 * D, D, **e))
-            self.register_buffer(f"b_mod_{s}", torch.empty(6 * D, **e))
+        self.mod_off = mod_off
+        for j, s in enumerate(("img", "txt")):
+            o = mod_off + j * 6 * D
+            self.register_buffer(f"w_mod_{s}", mod_w[o:o + 6 * D] if mod_w is not None
+                                 else torch.empty(6 * D, D, **e))
+            self.register_buffer(f"b_mod_{s}", mod_b[o:o + 6 * D] if mod_b is not None
+                                 else torch.empty(6 * D, **e))
             self.register_buffer(f"w_qkv_{s}", lin(3 * D, D))
             self.register_buffer(f"b_qkv_{s}", torch.empty(3 * D, **e))
             self.register_buffer(f"w_out_{s}", lin(D, D))
@@ -119,6 +127,8 @@ class _Workspace:
         self.stemb = torch.empty(B, D, **e)
         self.mod_img = torch.empty(B, 6 * D, **e)
         self.mod_txt = torch.empty(B, 6 * D, **e)
+        # every block's img/txt modulation vectors, from one GEMV launch per forward
+        self.mod_all = torch.empty(B, cfg.num_layers * 2 * 6 * D, **e)
         self.emb_out = torch.empty(B, 2 * D, **e)
         self.t_bf = torch.empty(B, **e)
         if int8:
@@ -166,8 +176,15 @@ class QwenImageTransformer2DModel(nn.Module):
         self.register_buffer("norm_out_b", torch.empty(2 * D, **e))
         self.register_buffer("proj_out_w", torch.empty(P, D, **e))
         self.register_buffer("proj_out_b", torch.empty(P, **e))
-        self.transformer_blocks = nn.ModuleList(_Block(D, Dh, F, device, int8_only=int8_only)
-                                                for _ in range(num_layers))
+        # AdaLN modulation weights of all blocks packed [L * 2 * 6D, D] (block-major, img then txt):
+        # the per-block w_mod_* buffers are views, and one GEMV produces every block's modulation
+        # vectors at the top of the forward (13.6 GB streamed in one launch that fills the chip,
+        # instead of 120 launches of 113 MB each on the blocks' critical path)
+        self._mod_w = torch.empty(num_layers * 12 * D, D, **e)
+        self._mod_b = torch.empty(num_layers * 12 * D, **e)
+        self.transformer_blocks = nn.ModuleList(
+            _Block(D, Dh, F, device, int8_only=int8_only, mod_w=self._mod_w, mod_b=self._mod_b,
+                   mod_off=i * 12 * D) for i in range(num_layers))
         self.int8 = False
         self.int8_only = int8_only
         # optional kernel probe: {"attention": [...], "mlp_up": [...]} lists of
@@ -191,6 +208,9 @@ class QwenImageTransformer2DModel(nn.Module):
         # their one bf16 rounding) and the attention takes log2-unit logits straight from the
         # MFMA (qie_attention_fwd_log2q_bf16); False: plain q, scale inside (A/B switch)
         self.log2q_attention = True
+        # all 120 modulation GEMVs as one launch before the blocks; False: one launch per block and
+        # stream, inside the block (A/B switch)
+        self.batched_modulation = True
         # K % 64 requirement of the GEMM kernels for the small input projections
         if in_channels % 64 or joint_attention_dim % 64:
             raise NotImplementedError("in_channels and joint_attention_dim must be multiples of 64")
@@ -470,6 +490,8 @@ class QwenImageTransformer2DModel(nn.Module):
         ops.silu(ws.t_h, out=ws.t_hs)
         ops.gemv(ws.t_hs, self.t_l2_w, self.t_l2_b, out=ws.temb)
         ops.silu(ws.temb, out=ws.stemb)
+        if self.batched_modulation:
+            ops.gemv(ws.stemb, self._mod_w, self._mod_b, out=ws.mod_all)
         kv_len = [S_img + l for l in txt_lens]
         side = self._side_stream() if has_txt else None
         if side is not None:  # the text stream starts from the prologue's x_txt and stemb
@@ -506,8 +528,13 @@ class QwenImageTransformer2DModel(nn.Module):
         R_t = B * S_txt
         has_txt = S_txt > 0
         main = torch.cuda.current_stream() if side is not None else None
-        img = ("img", ws.x_img, ws.h_img, ws.att_img, ws.mlp_img, ws.mod_img, S_img, 0)
-        txt = ("txt", ws.x_txt[:R_t], ws.h_txt[:R_t], ws.att_txt[:R_t], ws.mlp_txt[:R_t], ws.mod_txt,
+        if self.batched_modulation:
+            D6, o = 6 * self.config.inner_dim, blk.mod_off
+            m_img, m_txt = ws.mod_all[:, o:o + D6], ws.mod_all[:, o + D6:o + 2 * D6]
+        else:
+            m_img, m_txt = ws.mod_img, ws.mod_txt
+        img = ("img", ws.x_img, ws.h_img, ws.att_img, ws.mlp_img, m_img, S_img, 0)
+        txt = ("txt", ws.x_txt[:R_t], ws.h_txt[:R_t], ws.att_txt[:R_t], ws.mlp_txt[:R_t], m_txt,
                S_txt, S_img)
         # ---- modulation, LN1 + modulate, fused QKV projection, QK RMSNorm + RoPE
         if has_txt:
@@ -537,7 +564,8 @@ class QwenImageTransformer2DModel(nn.Module):
         stream's rows of the joint qkv buffer; per-head RMSNorm + RoPE of q and k."""
         s, x, h, att, mlp, m, rpb, seq_off = st
         D = self.config.inner_dim
-        ops.gemv(ws.stemb, getattr(blk, f"w_mod_{s}"), getattr(blk, f"b_mod_{s}"), out=m)
+        if not self.batched_modulation:
+            ops.gemv(ws.stemb, getattr(blk, f"w_mod_{s}"), getattr(blk, f"b_mod_{s}"), out=m)
         # chunks of m: shift1 scale1 gate1 shift2 scale2 gate2
         nq, nk = (blk.norm_q, blk.norm_k) if s == "img" else (blk.norm_added_q, blk.norm_added_k)
         if self.int8:

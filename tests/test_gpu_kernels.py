@@ -69,7 +69,8 @@ def test_linear_strided_input(dev):
     close(ops.linear(x, w, b), R.linear(x.cpu(), w.cpu(), b.cpu(), RB))
 
 
-@pytest.mark.parametrize("M,N,K", [(1, 18432, 3072), (2, 6144, 3072), (4, 3072, 256), (9, 512, 1024)])
+@pytest.mark.parametrize("M,N,K", [(1, 18432, 3072), (2, 18432, 3072), (2, 6144, 3072), (4, 3072, 256), (9, 512, 1024),
+                                   (2, 100, 1000), (3, 37, 4168)])
 def test_gemv(dev, M, N, K):
     ops = _ops()
     x, w, b = rnd((M, K), dev, 1.0, 7), rnd((N, K), dev, 0.02, 8), rnd((N,), dev, 0.02, 9)

@@ -63,6 +63,25 @@ def test_tiny_forward_vs_oracle(dev, tiny):
     assert torch.equal(out0, out[:1])
 
 
+def test_batched_modulation_bitwise(dev, tiny):
+    """One GEMV launch for every block's modulation == one launch per block and stream, bit for
+    bit (each output column is the same wave's arithmetic either way); the per-block w_mod_*
+    buffers are views of the packed [L * 12D, D] matrix the batched launch reads."""
+    cfg, params, m = tiny
+    blk = m.transformer_blocks[1]
+    assert blk.w_mod_txt.data_ptr() == m._mod_w[blk.mod_off + 6 * m.config.inner_dim:].data_ptr()
+    shapes = [(1, 8, 8), (1, 8, 8)]
+    hs, enc = _inputs(2, shapes, 16, cfg.joint_attention_dim, seed=5)
+    t = R.model_timestep(torch.tensor([1000.0, 500.0]))
+    outs = []
+    for batched in (True, False):
+        m.batched_modulation = batched
+        outs.append(m(hs.to(dev), enc.to(dev), None, t.to(dev), [shapes] * 2, [16, 16],
+                      return_dict=False)[0].clone())
+    m.batched_modulation = True
+    assert torch.equal(outs[0], outs[1])
+
+
 def test_full_width_block_vs_oracle(dev):
     cfg = R.DiTConfig(num_layers=1)
     params = R.random_params(cfg, seed=1)
