@@ -445,6 +445,9 @@ struct Mma4<true> {
 // also applies the per-head RMSNorm (fp32 sum of squares over the head's 128 columns: the wave's
 // 64 + its partner wave's 64, exchanged through `smem`) and the RoPE rotation of q and k, with
 // the rounding points of qie_qk_norm_rope_bf16; it needs every wave of the workgroup here.
+#ifndef QIE_GATE_UNIFORM  // gated-residual epilogue: one gate load + 8-row residual round trip
+#define QIE_GATE_UNIFORM 1
+#endif
 template <int NT, int EPI, bool I8>
 __device__ __forceinline__ void ring_epilogue(typename MfmaOp<I8>::acc (&acc)[8][NT], const EpiArgs& e, int M,
                                               int N, int mrow0, int ncol0, int lane, char QIE_LDS* smem) {
@@ -570,6 +573,48 @@ __device__ __forceinline__ void ring_epilogue(typename MfmaOp<I8>::acc (&acc)[8]
     }
   }
   if constexpr (EPI == EPI_GATE_RES && NT == 4) {
+#if QIE_GATE_UNIFORM
+    // the wave's 128 rows in one batch (wave-uniform; always so for the image rows, S_img % 128 ==
+    // 0): one gate vector for all of them, so the residual loads of all 8 row groups fit the
+    // registers the 4-row form spends on residual + gate, and go out in one round trip
+    const int b0 = min(mrow0, M - 1) / e.rows_per_batch;
+    if (b0 == min(mrow0 + 127, M - 1) / e.rows_per_batch) {
+      u32x4_t gv[2], xv[8][2];
+#pragma unroll
+      for (int jp = 0; jp < 2; ++jp) {
+        const int n = min(ncol0 + jp * 32 + (g & 1) * 16 + (g >> 1) * 8, N - 8);
+        gv[jp] = *(const u32x4_t*)(e.gate + (int64_t)b0 * e.gate_bstride + n);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int mc = min(mrow0 + i * 16 + fr, M - 1);
+          xv[i][jp] = *(const u32x4_t*)((const bf16_t*)e.out + (int64_t)mc * e.ldo + n);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int m = mrow0 + i * 16 + fr;
+        const int mc = min(m, M - 1);
+#pragma unroll
+        for (int jp = 0; jp < 2; ++jp) {
+          const int nb = ncol0 + jp * 32;
+          u32x2_t a = epi_pre<EPI, I8>(e, mc, min(nb + g * 4, N - 4), acc[i][2 * jp]);
+          u32x2_t b = epi_pre<EPI, I8>(e, mc, min(nb + 16 + g * 4, N - 4), acc[i][2 * jp + 1]);
+          const auto sx = __builtin_amdgcn_permlane16_swap(a.x, b.x, false, false);
+          const auto sy = __builtin_amdgcn_permlane16_swap(a.y, b.y, false, false);
+          const uint32_t vv[4] = {sx[0], sy[0], sx[1], sy[1]};
+          const uint32_t gg[4] = {gv[jp].x, gv[jp].y, gv[jp].z, gv[jp].w};
+          const uint32_t xx[4] = {xv[i][jp].x, xv[i][jp].y, xv[i][jp].z, xv[i][jp].w};
+          uint32_t o[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            o[k] = pack2(lo_f(xx[k]) + rbf(lo_f(gg[k]) * lo_f(vv[k])), hi_f(xx[k]) + rbf(hi_f(gg[k]) * hi_f(vv[k])));
+          const int n = nb + (g & 1) * 16 + (g >> 1) * 8;
+          if (m < M && n < N) *(u32x4_t*)((bf16_t*)e.out + (int64_t)m * e.ldo + n) = u32x4_t{o[0], o[1], o[2], o[3]};
+        }
+      }
+      return;
+    }
+#endif
     // x is read and written in place, so hipcc cannot hoist a later row's residual load above an
     // earlier row's store: issue the residual and gate loads of 4 rows first, then combine and
     // store (one round trip per 4 rows instead of one per 16-byte chunk)

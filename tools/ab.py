@@ -101,7 +101,8 @@ def main():
         w = (torch.randn(N, K, device=dev) * 0.02).to(BF16)
         b = torch.zeros(N, device=dev, dtype=BF16)
         gate = (torch.randn(2, 6 * N, device=dev) * 0.1).to(BF16)
-        outs = [torch.randn(M, N, device=dev).to(BF16) for _ in libs]
+        r0 = torch.randn(M, N, device=dev).to(BF16)  # the same start residual for every build
+        outs = [r0.clone() for _ in libs]
         flops = 2.0 * M * N * K
         for lib in libs:
             lib.qie_linear_gated_residual_bf16.argtypes = [
