@@ -445,6 +445,9 @@ struct Mma4<true> {
 // also applies the per-head RMSNorm (fp32 sum of squares over the head's 128 columns: the wave's
 // 64 + its partner wave's 64, exchanged through `smem`) and the RoPE rotation of q and k, with
 // the rounding points of qie_qk_norm_rope_bf16; it needs every wave of the workgroup here.
+#ifndef QIE_NR_HOIST  // QKV + norm + RoPE epilogue: RoPE table loads of 4 row groups ahead of their stores
+#define QIE_NR_HOIST 1
+#endif
 #ifndef QIE_GATE_UNIFORM  // gated-residual epilogue: one gate load + 8-row residual round trip
 #define QIE_GATE_UNIFORM 1
 #endif
@@ -536,12 +539,33 @@ __device__ __forceinline__ void ring_epilogue(typename MfmaOp<I8>::acc (&acc)[8]
             const int d0 = dbase + jp * 32 + dl;
             const u32x4_t ww = *(const u32x4_t*)(nw + d0);
             const uint32_t wv[4] = {ww.x, ww.y, ww.z, ww.w};
+#if QIE_NR_HOIST
+            // the RoPE rows of 4 row groups loaded before their stores: hipcc may not move a table
+            // load above a store to the qkv buffer (possible alias), so in loop order every row's
+            // cos/sin would be a separate round trip
 #pragma unroll
-            for (int i = 0; i < 8; ++i) {
-              const int m = mrow0 + i * 16 + fr;
-              const int sl = min(m, M - 1) % e.rows_per_batch;  // row of the segment's RoPE table
-              const f32x4_t cs = *(const f32x4_t*)(e.rcos + (int64_t)sl * 64 + (d0 >> 1));
-              const f32x4_t sn = *(const f32x4_t*)(e.rsin + (int64_t)sl * 64 + (d0 >> 1));
+            for (int i4 = 0; i4 < 8; i4 += 4) {
+              f32x4_t csv[4], snv[4];
+#pragma unroll
+              for (int ii = 0; ii < 4; ++ii) {
+                const int sl = min(mrow0 + (i4 + ii) * 16 + fr, M - 1) % e.rows_per_batch;
+                csv[ii] = *(const f32x4_t*)(e.rcos + (int64_t)sl * 64 + (d0 >> 1));
+                snv[ii] = *(const f32x4_t*)(e.rsin + (int64_t)sl * 64 + (d0 >> 1));
+              }
+#pragma unroll
+              for (int ii = 0; ii < 4; ++ii) {
+                const int i = i4 + ii;
+                const int m = mrow0 + i * 16 + fr;
+                const f32x4_t cs = csv[ii], sn = snv[ii];
+#else
+            {
+#pragma unroll
+              for (int i = 0; i < 8; ++i) {
+                const int m = mrow0 + i * 16 + fr;
+                const int sl = min(m, M - 1) % e.rows_per_batch;  // row of the segment's RoPE table
+                const f32x4_t cs = *(const f32x4_t*)(e.rcos + (int64_t)sl * 64 + (d0 >> 1));
+                const f32x4_t sn = *(const f32x4_t*)(e.rsin + (int64_t)sl * 64 + (d0 >> 1));
+#endif
               const u32x4_t v = cols8(i, jp);
               const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
               uint32_t o[4];
@@ -552,6 +576,7 @@ __device__ __forceinline__ void ring_epilogue(typename MfmaOp<I8>::acc (&acc)[8]
                 o[k] = pack2((x0 * cs[k] - x1 * sn[k]) * osc, (x0 * sn[k] + x1 * cs[k]) * osc);
               }
               if (m < M) *(u32x4_t*)(row_ptr(m) + jp * 32) = u32x4_t{o[0], o[1], o[2], o[3]};
+              }
             }
           }
           done = true;

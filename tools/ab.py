@@ -113,6 +113,27 @@ def main():
             rc = libs[i].qie_linear_gated_residual_bf16(x.data_ptr(), K, w.data_ptr(), b.data_ptr(), gate.data_ptr(),
                                                         6 * N, M // 2, outs[i].data_ptr(), N, M, N, K, st)
             assert rc == 0, rc
+    elif what == "qkvnr":  # image QKV GEMM + QK RMSNorm + RoPE epilogue, headline shape (B = 2, S_img 8192)
+        B, H, Dh, S_IMG, S_PAD, K = 2, 24, 128, 8192, 8448, 3072
+        M, N = B * S_IMG, 3 * H * Dh
+        x = torch.randn(M, K, device=dev).to(BF16)
+        w = (torch.randn(N, K, device=dev) * 0.02).to(BF16)
+        b = torch.zeros(N, device=dev, dtype=BF16)
+        nq, nk = (1 + 0.1 * torch.randn(2, Dh, device=dev)).to(BF16)
+        ang = torch.randn(S_IMG, Dh // 2, device=dev)
+        cos_t, sin_t = ang.cos().contiguous(), ang.sin().contiguous()
+        outs = [torch.zeros(3, B, H, S_PAD, Dh, device=dev, dtype=BF16) for _ in libs]
+        flops = 2.0 * M * N * K
+        for lib in libs:
+            lib.qie_linear_qkv_norm_rope_bf16.argtypes = [
+                ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p] + \
+                [ctypes.c_int] * 8 + [ctypes.c_void_p] * 4 + [ctypes.c_float, ctypes.c_float, ctypes.c_void_p]
+
+        def run(i):
+            rc = libs[i].qie_linear_qkv_norm_rope_bf16(
+                x.data_ptr(), K, w.data_ptr(), b.data_ptr(), outs[i].data_ptr(), M, K, S_IMG, 0, B, H, Dh, S_PAD,
+                nq.data_ptr(), nk.data_ptr(), cos_t.data_ptr(), sin_t.data_ptr(), 1e-6, 1.0, st)
+            assert rc == 0, rc
     elif what.startswith("gemm"):
         if what.startswith("gemm:"):  # gemm:M:N:K
             M, N, K = (int(v) for v in what.split(":")[1:])
