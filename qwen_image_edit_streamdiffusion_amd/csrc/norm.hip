@@ -36,6 +36,9 @@ __device__ __forceinline__ u32x2_t quant8(const float f[8], float inv) {
   return u32x2_t{w[0], w[1]};
 }
 
+#ifndef QIE_LNMOD_PREFETCH
+#define QIE_LNMOD_PREFETCH 0  // measured slower: 42.0 vs 39.3 us (register pressure), kept as a build option
+#endif
 template <bool I8>
 __global__ void __launch_bounds__(256)
     ln_mod_kernel(const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __restrict__ shift,
@@ -57,6 +60,20 @@ __global__ void __launch_bounds__(256)
       for (int j = 0; j < 8; ++j) sum += v[i][j];
     }
   }
+  const int b = row / rpb;
+  const bf16_t* sh = shift + (int64_t)b * mod_bstride;
+  const bf16_t* sc = scale + (int64_t)b * mod_bstride;
+#if QIE_LNMOD_PREFETCH
+  // scale / shift issued with x, under the two reductions: in the store loop below hipcc may not
+  // move chunk i+1's loads above chunk i's store (y may alias them), one round trip per chunk
+  u32x4_t scv[kMaxC], shv[kMaxC];
+#pragma unroll
+  for (int i = 0; i < kMaxC; ++i) {
+    const int c = min(lane + 64 * i, nch - 1);
+    scv[i] = *(const u32x4_t*)(sc + c * 8);
+    shv[i] = *(const u32x4_t*)(sh + c * 8);
+  }
+#endif
   const float mean = wave_sum(sum) / (float)D;
   float sq = 0.f;
 #pragma unroll
@@ -68,17 +85,19 @@ __global__ void __launch_bounds__(256)
         sq += d * d;
       }
   const float rstd = rsqrtf(wave_sum(sq) / (float)D + eps);
-  const int b = row / rpb;
-  const bf16_t* sh = shift + (int64_t)b * mod_bstride;
-  const bf16_t* sc = scale + (int64_t)b * mod_bstride;
   float amax = 0.f;
 #pragma unroll
   for (int i = 0; i < kMaxC; ++i) {
     const int c = lane + 64 * i;
     if (c < nch) {
       float s8[8], h8[8];
+#if QIE_LNMOD_PREFETCH
+      unpack8(scv[i], s8);
+      unpack8(shv[i], h8);
+#else
       unpack8(*(const u32x4_t*)(sc + c * 8), s8);
       unpack8(*(const u32x4_t*)(sh + c * 8), h8);
+#endif
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float n = rbf((v[i][j] - mean) * rstd);

@@ -60,3 +60,12 @@ mod = torch.randn(2, 6 * D, device=dev).to(torch.bfloat16)
 o = torch.empty_like(h)
 t = bench(lambda: ops.layernorm_modulate(h, mod[:, :D], mod[:, D:2 * D], 8192, out=o))
 print(f"ln_mod rows={R} D={D}: {t:.1f} us, {2 * h.numel() * 2 / t / 1e6:.2f} TB/s")
+for so in sys.argv[1:]:  # the same A/B for qie_layernorm_modulate_bf16
+    lib = ctypes.CDLL(so)
+    lib.qie_layernorm_modulate_bf16.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
+                                                ctypes.c_int64, ctypes.c_int, ctypes.c_void_p, ctypes.c_int64,
+                                                ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_void_p]
+    st = torch.cuda.current_stream().cuda_stream
+    t2 = bench(lambda: lib.qie_layernorm_modulate_bf16(h.data_ptr(), D, mod.data_ptr(), mod[:, D:].data_ptr(),
+                                                       6 * D, 8192, o.data_ptr(), D, R, D, 1e-6, st))
+    print(f"  {so}: ln_mod {t2:.1f} us, {2 * h.numel() * 2 / t2 / 1e6:.2f} TB/s")
