@@ -60,54 +60,78 @@ def _worker_main(rank: int, device_index: Optional[int], loader_spec: str, do_wa
             res_q.put(("err", rank, f"{e}"))
 
 
+class WorkerDied(RuntimeError):
+    """The GPU worker serving a request exited (GPU fault, OOM kill) before it answered."""
+
+
 class GpuDispatcher:
     """``size`` worker processes (one per GPU, device ``devices[i]``), one request each.
 
     Same worker protocol as ``server.LocalWorker``: ``try_acquire() -> token | None``,
     ``run(token, image, request)`` (blocking, on ``executor``), ``release(token)``.
+
+    A worker that dies mid-request is detected while ``run`` waits (its process is polled every
+    ``poll`` seconds): the request fails with ``WorkerDied`` (HTTP 500), the death is recorded in
+    ``errors``, and a fresh ``spawn`` child is started for that GPU in the background (a new
+    process, never an exec of this one). The slot stays out of the free list until the new worker
+    reports ready, so a lost GPU never turns into a permanent 429.
     """
 
     def __init__(self, size: int, loader_spec: str, devices: Optional[List[Optional[int]]] = None,
-                 do_warmup: bool = True, start_timeout: float = 1800.0):
+                 do_warmup: bool = True, start_timeout: float = 1800.0, poll: float = 1.0,
+                 respawn: bool = True):
         self.size = size
         self.loader_spec = loader_spec
         self.devices = list(devices) if devices is not None else list(range(size))
         self.do_warmup = do_warmup
         self.start_timeout = start_timeout
+        self.poll = poll
+        self.respawn = respawn
         self.executor = ThreadPoolExecutor(max_workers=size)
         self._lock = threading.Lock()
         self._free: List[int] = []
+        self._down = set()  # slots whose worker died; not handed out until a replacement is ready
         self._procs = []
         self._req = []
         self._res = []
+        self._ctx = None
         self.errors = {}
+        self.restarts = 0
 
     @property
     def loaded(self) -> bool:
         return bool(self._procs) and len(self.errors) < self.size
 
+    def _spawn(self, r: int):
+        rq, sq = self._ctx.Queue(), self._ctx.Queue()
+        p = self._ctx.Process(target=_worker_main, args=(r, self.devices[r], self.loader_spec,
+                                                         self.do_warmup, rq, sq), daemon=True)
+        p.start()
+        return p, rq, sq
+
+    def _await_ready(self, r: int, sq) -> bool:
+        try:
+            kind, rank, msg = sq.get(timeout=self.start_timeout)
+        except queue.Empty:
+            kind, rank, msg = "dead", r, "timed out while loading"
+        if kind == "ready":
+            return True
+        self.errors[r] = msg
+        return False
+
     def start(self):
         import torch
         if torch.cuda.is_initialized():
             raise RuntimeError("GpuDispatcher.start() must run before this process touches the GPU")
-        ctx = mp.get_context("spawn")
+        self._ctx = mp.get_context("spawn")
         for r in range(self.size):
-            rq, sq = ctx.Queue(), ctx.Queue()
-            p = ctx.Process(target=_worker_main, args=(r, self.devices[r], self.loader_spec,
-                                                       self.do_warmup, rq, sq), daemon=True)
-            p.start()
+            p, rq, sq = self._spawn(r)
             self._procs.append(p)
             self._req.append(rq)
             self._res.append(sq)
         for r in range(self.size):
-            try:
-                kind, rank, msg = self._res[r].get(timeout=self.start_timeout)
-            except queue.Empty:
-                kind, rank, msg = "dead", r, "timed out while loading"
-            if kind == "ready":
-                self._free.append(rank)
-            else:
-                self.errors[rank] = msg
+            if self._await_ready(r, self._res[r]):
+                self._free.append(r)
 
     def try_acquire(self) -> Optional[int]:
         with self._lock:
@@ -115,11 +139,51 @@ class GpuDispatcher:
 
     def release(self, token: int):
         with self._lock:
-            self._free.append(token)
+            if token not in self._down:
+                self._free.append(token)
+
+    def _replace(self, token: int):
+        """Start a fresh worker for ``token``'s GPU; the slot returns to the pool once it is ready."""
+        import torch
+        if torch.cuda.is_initialized():  # spawn re-executes the interpreter: never from a GPU process
+            self.errors[token] = "worker died; not respawned (dispatcher process holds the GPU)"
+            return
+        p, rq, sq = self._spawn(token)
+        self._procs[token], self._req[token], self._res[token] = p, rq, sq
+        self.restarts += 1
+        if self._await_ready(token, sq):
+            with self._lock:
+                self.errors.pop(token, None)
+                self._down.discard(token)
+                self._free.append(token)
+
+    def _worker_died(self, token: int):
+        code = self._procs[token].exitcode
+        with self._lock:
+            self._down.add(token)
+        self.errors[token] = f"worker {token} died (exit code {code})"
+        try:
+            self._procs[token].join(timeout=1)
+        except Exception:
+            pass
+        if self.respawn:
+            threading.Thread(target=self._replace, args=(token,), daemon=True).start()
+        raise WorkerDied(self.errors[token])
 
     def run(self, token: int, image: Image.Image, req) -> Image.Image:
         self._req[token].put((_to_png(image), req.prompt, req.steps, req.use_cfg))
-        kind, _, payload = self._res[token].get()
+        res, proc = self._res[token], self._procs[token]
+        while True:
+            try:
+                kind, _, payload = res.get(timeout=self.poll)
+                break
+            except queue.Empty:
+                if not proc.is_alive():
+                    try:  # the answer may have landed just before the exit
+                        kind, _, payload = res.get(timeout=0.1)
+                        break
+                    except queue.Empty:
+                        self._worker_died(token)
         if kind != "ok":
             raise RuntimeError(payload)
         return _from_png(payload)

@@ -160,6 +160,9 @@ class QwenImageEditPlusPipeline:
 
     def load_lora_weights(self, pretrained_model_name_or_path_or_dict, weight_name: Optional[str] = None,
                           adapter_name: Optional[str] = None, lora_scale: float = 1.0, **kw) -> int:
+        """Fuse a LoRA file / state dict into the transformer (W += s*B@A); returns the adapter
+        count. Raises ``weights.LoraKeyError`` when no adapter fuses or a key maps onto no linear
+        (peft, diffusion_model.* lora_down/up and kohya lora_unet_* forms are all accepted)."""
         sd = pretrained_model_name_or_path_or_dict
         if not isinstance(sd, dict):
             sd = W.load_lora_file(sd, weight_name)

@@ -158,7 +158,9 @@ def load_pipeline_from_env(device: str = "cuda"):
     pipe = QwenImageEditPlusPipeline.from_pretrained(path, device=device)
     lora = os.environ.get("QIE_LORA_PATH")
     if lora:
-        pipe.load_lora_weights(lora, weight_name=os.environ.get("QIE_LORA_WEIGHT"))
+        # raises (and so fails start-up) when the file's keys do not map onto the transformer
+        n = pipe.load_lora_weights(lora, weight_name=os.environ.get("QIE_LORA_WEIGHT"))
+        print(f"LoRA: fused {n} adapters from {lora}", flush=True)
     if os.environ.get("QIE_INT8") == "1" and not pipe.transformer.int8:
         pipe.transformer.quantize_int8()
     enc = os.environ.get("QIE_ENCODERS")

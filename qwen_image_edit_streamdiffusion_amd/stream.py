@@ -72,9 +72,29 @@ class CachedConditions:
         self.negative_prompt_embeds: Optional[torch.Tensor] = None
         self.negative_prompt_embeds_mask: Optional[torch.Tensor] = None
         self.reference_latents: Optional[torch.Tensor] = None
+        self.reference_key: Optional[str] = None
+
+    @staticmethod
+    def image_key(image) -> Optional[str]:
+        """Content key of the image the prompt was encoded with (None: no image block)."""
+        if image is None:
+            return None
+        import hashlib
+        h = hashlib.sha1()
+        if isinstance(image, torch.Tensor):
+            h.update(str(tuple(image.shape)).encode())
+            h.update(image.detach().cpu().contiguous().numpy().tobytes())
+        else:
+            im = image.convert("RGB")
+            h.update(str(im.size).encode())
+            h.update(im.tobytes())
+        return h.hexdigest()
 
     def is_valid(self, prompt: str, reference_image=None) -> bool:
-        return self.prompt_embeds is not None and prompt == self.prompt
+        """qwen_realtime.py:82-89 keys on the prompt; the image block of the prompt is part of
+        the key too, so re-encoding with a new frame is not served from the cache."""
+        return (self.prompt_embeds is not None and prompt == self.prompt
+                and self.image_key(reference_image) == self.reference_key)
 
 
 class StreamBatchDenoiser:
@@ -262,6 +282,14 @@ class QwenRealtimePipeline:
     def precompute_conditions(self, prompt: str, reference_image=None, prompt_embeds=None,
                               prompt_embeds_mask=None, negative_prompt_embeds=None,
                               negative_prompt_embeds_mask=None):
+        """Encode the prompt once and build the stream engine (qwen_realtime.py:140-165).
+
+        Deliberate approximation: the reference's per-frame pipeline call encodes each camera
+        frame into the Qwen2.5-VL prompt ("Picture 1: <frame>"); here the prompt is encoded once,
+        with ``reference_image`` (usually None, so no image block), and every later frame reuses
+        those embeddings -- the frame still conditions the DiT through its VAE latents. Call this
+        again with ``reference_image=<frame>`` (e.g. on keyframes) to refresh the image block; the
+        prompt encoder's VLM / LRU caches keep that cheap."""
         if self.cache.is_valid(prompt, reference_image) and prompt_embeds is None:
             return
         if prompt_embeds is None:
@@ -273,6 +301,7 @@ class QwenRealtimePipeline:
                 negative_prompt_embeds, negative_prompt_embeds_mask = self.prompt_encoder(" ", reference_image)
         c = self.cache
         c.prompt, c.prompt_embeds, c.prompt_embeds_mask = prompt, prompt_embeds, prompt_embeds_mask
+        c.reference_key = c.image_key(reference_image)
         c.negative_prompt_embeds, c.negative_prompt_embeds_mask = negative_prompt_embeds, negative_prompt_embeds_mask
         oh, ow = self.config.output_size
         chh, cww = self.config.cond_size
@@ -292,6 +321,33 @@ class QwenRealtimePipeline:
             return noise
         return (self.prev_latent.float() + self.config.noise_strength * noise.float()).to(BF16)
 
+    def frame_to_rgb(self, frame) -> torch.Tensor:
+        """A camera frame as the uint8 RGB [1, H, W, 3] condition image the engine was built for.
+
+        qwen_realtime.py:239-243 first resizes every frame to (config.width, config.height) with
+        LANCZOS; Edit-Plus then resizes its VAE input to the 1024^2-area size of that aspect
+        (LANCZOS again), which is ``config.cond_size`` here -- so a 640x480 webcam frame becomes
+        512x512, then 1024x1024, and never changes the engine's token count. uint8 tensors must
+        already have the cond size."""
+        import numpy as np
+        from PIL import Image
+        ch, cw = self.config.cond_size
+        dev = self.transformer.device
+        if isinstance(frame, torch.Tensor):
+            t = frame if frame.dim() == 4 else frame[None]
+            if t.dtype != torch.uint8 or tuple(t.shape[1:]) != (ch, cw, 3):
+                raise ValueError(f"uint8 frames must be RGB [(1,) {ch}, {cw}, 3] (config.cond_size); "
+                                 f"got {tuple(frame.shape)} {frame.dtype}")
+            return t.to(dev).contiguous()
+        if isinstance(frame, np.ndarray):
+            frame = Image.fromarray(frame)
+        im = frame.convert("RGB")
+        if im.size != (self.config.width, self.config.height):
+            im = im.resize((self.config.width, self.config.height), Image.LANCZOS)
+        if im.size != (cw, ch):
+            im = im.resize((cw, ch), Image.LANCZOS)
+        return torch.from_numpy(np.asarray(im).copy())[None].to(dev)
+
     @torch.no_grad()
     def process_frame(self, frame) -> Optional[torch.Tensor]:
         """Push one frame (packed cond latents, or anything image_encoder accepts);
@@ -302,8 +358,7 @@ class QwenRealtimePipeline:
         elif self.image_encoder is not None:
             cond = self.image_encoder(frame)
         elif self.vae_encoder is not None:  # qwen_realtime.py:167-186 encode_image, on the HIP path
-            from .pipeline import images_to_rgb
-            cond = self.vae_encoder.encode(images_to_rgb(frame, self.transformer.device))
+            cond = self.vae_encoder.encode(self.frame_to_rgb(frame))
         else:
             raise NotImplementedError("frames must be packed latents, or set vae_encoder / image_encoder")
         noise = self.prepare_latent(cond)

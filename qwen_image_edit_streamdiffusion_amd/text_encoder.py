@@ -406,11 +406,13 @@ class QwenImageEditPromptEncoder:
         if image is None:
             return []
         imgs = image if isinstance(image, (list, tuple)) else [image]
+        from PIL import Image
         out = []
         for im in imgs:
             if hasattr(im, "resize") and hasattr(im, "size") and not torch.is_tensor(im):
+                # Edit-Plus resizes through VaeImageProcessor.resize, whose default is LANCZOS [U]
                 w, h = condition_size(*im.size)
-                out.append(im.resize((w, h)))
+                out.append(im.resize((w, h), Image.LANCZOS))
             else:
                 out.append(im)
         return out

@@ -61,50 +61,107 @@ def load_transformer_weights(model, path: str, strict: bool = True) -> int:
     return n
 
 
-_LORA_PATTERNS = [
-    # peft / diffusers style
-    (re.compile(r"^(?:transformer\.)?(.+)\.lora_A(?:\.default)?\.weight$"), "A"),
-    (re.compile(r"^(?:transformer\.)?(.+)\.lora_B(?:\.default)?\.weight$"), "B"),
-    # kohya-ish style
-    (re.compile(r"^(?:transformer\.|diffusion_model\.)?(.+)\.lora_down\.weight$"), "A"),
-    (re.compile(r"^(?:transformer\.|diffusion_model\.)?(.+)\.lora_up\.weight$"), "B"),
-    (re.compile(r"^(?:transformer\.|diffusion_model\.)?(.+)\.alpha$"), "alpha"),
+# Key forms a Qwen-Image LoRA file comes in (diffusers accepts all of them through
+# `_convert_non_diffusers_qwen_lora_to_diffusers` [U] before peft loads the adapters):
+#   peft / diffusers   [transformer.]<stem>.lora_A[.default].weight, .lora_B[...]
+#   ComfyUI / lightx2v [diffusion_model.]<stem>.lora_down.weight, .lora_up.weight, .alpha
+#   kohya              lora_unet_<stem with "." -> "_">.lora_down.weight, ...
+# The stem prefixes are stripped in every form; kohya stems are resolved against the
+# model's own module names (each "." of a diffusers stem read as "_").
+_LORA_PREFIXES = ("base_model.model.", "model.diffusion_model.", "diffusion_model.", "transformer.")
+_LORA_SUFFIXES = [
+    (re.compile(r"^(.+)\.lora_A(?:\.default)?\.weight$"), "A"),
+    (re.compile(r"^(.+)\.lora_B(?:\.default)?\.weight$"), "B"),
+    (re.compile(r"^(.+)\.lora_down\.weight$"), "A"),
+    (re.compile(r"^(.+)\.lora_up\.weight$"), "B"),
+    (re.compile(r"^(.+)\.lora\.down\.weight$"), "A"),
+    (re.compile(r"^(.+)\.lora\.up\.weight$"), "B"),
+    (re.compile(r"^(.+)\.alpha$"), "alpha"),
 ]
 
 
-def parse_lora(sd: Dict[str, torch.Tensor]) -> Dict[str, Dict[str, torch.Tensor]]:
-    """Group a LoRA state dict into {module_stem: {"A": [r,in], "B": [out,r], "alpha": ()}}."""
+class LoraKeyError(KeyError):
+    """A LoRA state dict that does not map onto the transformer's linears."""
+
+
+def _lora_stem(key: str):
+    """(stem, kind) of one LoRA tensor name, prefixes stripped; None when it is no LoRA key."""
+    k = key
+    stripped = True
+    while stripped:
+        stripped = False
+        for p in _LORA_PREFIXES:
+            if k.startswith(p):
+                k, stripped = k[len(p):], True
+    for pat, kind in _LORA_SUFFIXES:
+        m = pat.match(k)
+        if m:
+            return m.group(1), kind
+    return None
+
+
+def parse_lora(sd: Dict[str, torch.Tensor], known_stems: Optional[Iterable[str]] = None):
+    """Group a LoRA state dict into {module_stem: {"A": [r,in], "B": [out,r], "alpha": ()}}.
+
+    Returns (groups, unparsed_keys). ``known_stems`` (the model's diffusers module names)
+    resolves kohya ``lora_unet_*`` stems, whose dots are underscores."""
+    flat = {s.replace(".", "_"): s for s in (known_stems or ())}
     groups: Dict[str, Dict[str, torch.Tensor]] = {}
+    unparsed = []
     for k, v in sd.items():
-        for pat, kind in _LORA_PATTERNS:
-            m = pat.match(k)
-            if m:
-                groups.setdefault(m.group(1), {})[kind] = v
-                break
-    return groups
+        r = _lora_stem(k)
+        if r is None:
+            unparsed.append(k)
+            continue
+        stem, kind = r
+        if stem.startswith("lora_unet_"):
+            stem = flat.get(stem[len("lora_unet_"):], stem)
+        groups.setdefault(stem, {})[kind] = v
+    return groups, unparsed
+
+
+def _linear_stems(model):
+    return sorted({n[:-len(".weight")] for n in model.diffusers_names() if n.endswith(".weight")})
 
 
 @torch.no_grad()
-def fuse_lora(model, lora_sd: Dict[str, torch.Tensor], scale: float = 1.0, strict: bool = False) -> int:
-    """W[stem] += scale * (alpha / r) * B @ A for every adapter in the dict."""
-    fused = 0
-    for stem, g in parse_lora(lora_sd).items():
+def fuse_lora(model, lora_sd: Dict[str, torch.Tensor], scale: float = 1.0, strict: bool = True) -> int:
+    """W[stem] += scale * (alpha / r) * B @ A for every adapter in the dict; returns the count.
+
+    Raises ``LoraKeyError`` when nothing fuses, and -- with ``strict`` (the default, as the
+    reference's diffusers loader refuses a state dict with keys left over after conversion) --
+    when a key is no LoRA key, an adapter lacks its A or B half, or a stem names no linear of
+    the model. ``strict=False`` skips those instead. A shape mismatch always raises."""
+    groups, unparsed = parse_lora(lora_sd, _linear_stems(model))
+    problems = [f"not a LoRA key: {k}" for k in unparsed]
+    todo = []
+    for stem, g in groups.items():
         if "A" not in g or "B" not in g:
+            problems.append(f"{stem}: lora {'B' if 'A' in g else 'A'} half missing")
             continue
         try:
             w = model._param_slot(stem + ".weight")
-        except (KeyError, IndexError, AttributeError):
-            if strict:
-                raise
+        except (KeyError, IndexError, AttributeError, ValueError):
+            problems.append(f"{stem}: no such linear in the transformer")
             continue
+        A, B = g["A"], g["B"]
+        if A.dim() != 2 or B.dim() != 2 or A.shape[0] != B.shape[1] or (B.shape[0], A.shape[1]) != tuple(w.shape):
+            raise LoraKeyError(f"{stem}: lora A {tuple(A.shape)} / B {tuple(B.shape)} do not fit weight "
+                               f"{tuple(w.shape)}")
+        todo.append((stem, w, g))
+    if problems and strict:
+        raise LoraKeyError(f"{len(problems)} LoRA entries do not map onto the transformer, e.g. "
+                           f"{problems[:3]}")
+    if not todo:
+        raise LoraKeyError(f"no LoRA adapter fused ({len(lora_sd)} keys; {problems[:3]})")
+    for stem, w, g in todo:
         A = g["A"].to(model.device, torch.float32)
         B = g["B"].to(model.device, torch.float32)
         r = A.shape[0]
         s = scale * (float(g["alpha"]) / r if "alpha" in g else 1.0)
         w.copy_((w.float() + s * (B @ A)).to(BF16))
-        fused += 1
     model._requantize_if_needed()
-    return fused
+    return len(todo)
 
 
 def load_lora_file(path: str, weight_name: Optional[str] = None) -> Dict[str, torch.Tensor]:

@@ -13,13 +13,17 @@ class _Out:
 class StubPipeline:
     """Records every call; returns the inverted input image after ``delay`` seconds."""
 
-    def __init__(self, delay: float = 0.0, fail: str = ""):
+    def __init__(self, delay: float = 0.0, fail: str = "", die_on: str = ""):
         self.calls = []
         self.delay = delay
         self.fail = fail
+        self.die_on = die_on
 
     def __call__(self, **kw):
         self.calls.append(kw)
+        if self.die_on and kw.get("prompt") == self.die_on:
+            import os
+            os._exit(3)  # a worker lost mid-request (GPU fault / OOM kill stand-in)
         if self.fail:
             raise ValueError(self.fail)
         if self.delay:
@@ -29,6 +33,10 @@ class StubPipeline:
 
 def load_stub():
     return StubPipeline(delay=1.5)
+
+
+def load_dying_stub():
+    return StubPipeline(delay=0.2, die_on="die")
 
 
 def solid(color, size=(64, 48)):

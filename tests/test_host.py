@@ -113,14 +113,74 @@ def test_lora_fuse_on_packed_slices():
     A, B = torch.randn(4, D, generator=g) * 0.1, torch.randn(D, 4, generator=g) * 0.1
     sd = {"transformer_blocks.1.attn.add_q_proj.lora_down.weight": A,
           "transformer_blocks.1.attn.add_q_proj.lora_up.weight": B,
-          "transformer_blocks.1.attn.add_q_proj.alpha": torch.tensor(2.0),
-          "unrelated.lora_A.weight": torch.zeros(1, 1)}
+          "transformer_blocks.1.attn.add_q_proj.alpha": torch.tensor(2.0)}
     assert W.fuse_lora(m, sd, scale=1.0) == 1
     exp = (params["transformer_blocks.1.attn.add_q_proj.weight"].float() + 0.5 * (B @ A)).to(BF16)
     assert torch.equal(m.transformer_blocks[1].w_qkv_txt[:D], exp)
     # the neighbouring k slice is untouched
     assert torch.equal(m.transformer_blocks[1].w_qkv_txt[D:2 * D],
                        params["transformer_blocks.1.attn.add_k_proj.weight"])
+
+
+_LORA_FORMS = {
+    # peft / diffusers (transformer. prefix, optional .default adapter name)
+    "peft": ("transformer.{s}.lora_A.weight", "transformer.{s}.lora_B.weight", None),
+    "peft_default": ("{s}.lora_A.default.weight", "{s}.lora_B.default.weight", None),
+    # lightx2v / ComfyUI: diffusion_model. prefix on either naming
+    "comfy_AB": ("diffusion_model.{s}.lora_A.weight", "diffusion_model.{s}.lora_B.weight", None),
+    "comfy_updown": ("diffusion_model.{s}.lora_down.weight", "diffusion_model.{s}.lora_up.weight",
+                     "diffusion_model.{s}.alpha"),
+    # kohya: lora_unet_ + the stem with every "." as "_"
+    "kohya": ("lora_unet_{u}.lora_down.weight", "lora_unet_{u}.lora_up.weight", "lora_unet_{u}.alpha"),
+}
+
+
+@pytest.mark.parametrize("form", sorted(_LORA_FORMS))
+@pytest.mark.parametrize("stem", ["transformer_blocks.0.attn.to_out.0", "transformer_blocks.1.img_mlp.net.0.proj",
+                                  "transformer_blocks.1.attn.add_k_proj", "transformer_blocks.0.txt_mod.1"])
+def test_lora_key_forms_fuse(form, stem):
+    cfg = R.tiny_config()
+    params = R.random_params(cfg, seed=5)
+    _, m = _tiny_cpu_model(params)
+    w0 = params[stem + ".weight"]
+    g = torch.Generator().manual_seed(2)
+    A = torch.randn(4, w0.shape[1], generator=g) * 0.1
+    B = torch.randn(w0.shape[0], 4, generator=g) * 0.1
+    ka, kb, kal = _LORA_FORMS[form]
+    sub = dict(s=stem, u=stem.replace(".", "_"))
+    sd = {ka.format(**sub): A, kb.format(**sub): B}
+    s = 1.0
+    if kal:
+        sd[kal.format(**sub)] = torch.tensor(8.0)
+        s = 2.0
+    assert W.fuse_lora(m, sd) == 1
+    exp = (w0.float() + s * (B @ A)).to(BF16)
+    assert torch.equal(m._param_slot(stem + ".weight"), exp)
+
+
+def test_lora_rejects_unmapped_keys():
+    cfg = R.tiny_config()
+    _, m = _tiny_cpu_model(R.random_params(cfg, seed=5))
+    D = cfg.inner_dim
+    A, B = torch.zeros(4, D), torch.zeros(D, 4)
+    good = {"transformer_blocks.0.attn.to_q.lora_A.weight": A, "transformer_blocks.0.attn.to_q.lora_B.weight": B}
+    # nothing maps: always an error, strict or not
+    bad = {"single_blocks.0.linear.lora_A.weight": A, "single_blocks.0.linear.lora_B.weight": B}
+    for strict in (True, False):
+        with pytest.raises(W.LoraKeyError):
+            W.fuse_lora(m, bad, strict=strict)
+    with pytest.raises(W.LoraKeyError):
+        W.fuse_lora(m, {}, strict=False)
+    # a half-adapter or a stray key: error when strict, skipped otherwise
+    for extra in ({"transformer_blocks.0.attn.to_k.lora_A.weight": A}, {"some.other.tensor": A},
+                  bad):
+        with pytest.raises(W.LoraKeyError):
+            W.fuse_lora(m, {**good, **extra})
+        assert W.fuse_lora(m, {**good, **extra}, strict=False) == 1
+    # shapes that do not fit the weight: always an error
+    with pytest.raises(W.LoraKeyError):
+        W.fuse_lora(m, {"transformer_blocks.0.attn.to_q.lora_A.weight": torch.zeros(4, D + 1),
+                        "transformer_blocks.0.attn.to_q.lora_B.weight": B}, strict=False)
 
 
 def test_ops_reject_host_tensors():
@@ -203,3 +263,36 @@ def test_stream_slots_fill_steady_flush(cpu_ops, steps, cfg_scale):
     for fid, lat in got:
         ref = _serial(tf, frames[fid][0], frames[fid][1], steps, cfg_scale, pe, ne)
         assert torch.equal(lat, ref), fid
+
+
+def test_realtime_frame_resize_non_square():
+    """a 640x480 webcam frame goes to (width, height) with LANCZOS first
+    (qwen_realtime.py:239-243), then to the engine's cond size -- never 1184x896."""
+    from PIL import Image
+    cfg = stream.StreamConfig()
+    rt = stream.QwenRealtimePipeline(cfg)
+    rt.transformer = type("T", (), {"device": torch.device("cpu")})()
+    rng = np.random.default_rng(0)
+    frame = Image.fromarray(rng.integers(0, 255, (480, 640, 3), dtype=np.uint8))
+    t = rt.frame_to_rgb(frame)
+    ch, cw = cfg.cond_size
+    assert t.dtype == torch.uint8 and tuple(t.shape) == (1, ch, cw, 3)
+    exp = frame.resize((cfg.width, cfg.height), Image.LANCZOS).resize((cw, ch), Image.LANCZOS)
+    assert np.array_equal(t[0].numpy(), np.asarray(exp))
+    # numpy frames (OpenCV-style RGB arrays) take the same path
+    assert torch.equal(rt.frame_to_rgb(np.asarray(frame)), t)
+    # uint8 tensors must already be at the cond size
+    assert torch.equal(rt.frame_to_rgb(t[0]), t)
+    with pytest.raises(ValueError):
+        rt.frame_to_rgb(torch.zeros(480, 640, 3, dtype=torch.uint8))
+
+
+def test_prompt_cache_keys_on_reference_image():
+    from PIL import Image
+    c = stream.CachedConditions()
+    c.prompt, c.prompt_embeds = "p", torch.zeros(1)
+    assert c.is_valid("p") and not c.is_valid("q")
+    a, b = Image.new("RGB", (8, 8), "red"), Image.new("RGB", (8, 8), "blue")
+    assert not c.is_valid("p", a)
+    c.reference_key = c.image_key(a)
+    assert c.is_valid("p", Image.new("RGB", (8, 8), "red")) and not c.is_valid("p", b)

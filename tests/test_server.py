@@ -152,3 +152,23 @@ def test_gpu_dispatcher_two_workers_cpu():
         assert r3.status_code == 429
         assert res[0].status_code == 200 and res[1].status_code == 200
         assert decode_b64(res[0].json()["image"]).size == (512, 512)
+
+
+def test_gpu_dispatcher_worker_death_is_500_and_respawned():
+    """a worker that dies mid-request fails that request with 500 (not a hang),
+    is recorded in the health errors, and a fresh worker takes its slot (no permanent 429)."""
+    import time
+    from qwen_image_edit_streamdiffusion_amd.dispatch import GpuDispatcher
+    d = GpuDispatcher(1, "server_stubs:load_dying_stub", devices=[None], do_warmup=False,
+                      start_timeout=300, poll=0.2)
+    with TestClient(S.create_app(dispatcher=d)) as c:
+        r = c.post("/edit", json={"image": b64_png(solid("gray")), "prompt": "die"})
+        assert r.status_code == 500 and "died" in r.json()["detail"]
+        for _ in range(600):  # the replacement loads in the background
+            if d.restarts == 1 and not d.errors and d.try_acquire() is not None:
+                d.release(0)
+                break
+            time.sleep(0.1)
+        assert d.restarts == 1 and not d.errors
+        r = c.post("/edit", json={"image": b64_png(solid("gray")), "prompt": "ok"})
+        assert r.status_code == 200

@@ -190,3 +190,29 @@ def test_prompt_hook_cache():
     assert len(calls) == 3
     hook("x", a)  # evicted by the bound of 2
     assert len(calls) == 4
+
+
+def test_condition_image_resized_lanczos():
+    """the processor gets the condition image resized with LANCZOS (Edit-Plus'
+    VaeImageProcessor.resize default), not PIL's default BICUBIC."""
+    import numpy as np
+    from PIL import Image
+    from qwen_image_edit_streamdiffusion_amd.text_encoder import QwenImageEditPromptEncoder
+    seen = {}
+
+    class Proc:
+        def __call__(self, text, images=None, return_tensors=None):
+            seen["images"] = images
+            return {"input_ids": torch.arange(80).view(1, -1)}
+
+    class Enc:
+        def __call__(self, ids, pv, grid):
+            return torch.zeros(ids.numel(), 4, dtype=torch.bfloat16)
+
+    rng = np.random.default_rng(1)
+    im = Image.fromarray(rng.integers(0, 255, (480, 640, 3), dtype=np.uint8))
+    QwenImageEditPromptEncoder(Enc(), Proc())("p", im)
+    got = np.asarray(seen["images"][0])
+    w, h = seen["images"][0].size
+    assert np.array_equal(got, np.asarray(im.resize((w, h), Image.LANCZOS)))
+    assert not np.array_equal(got, np.asarray(im.resize((w, h), Image.BICUBIC)))
