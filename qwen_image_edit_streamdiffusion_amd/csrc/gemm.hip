@@ -189,6 +189,55 @@ __device__ __forceinline__ u32x2_t epi_pre(const EpiArgs& e, int m, int n,
   return u32x2_t{pack2(v[0], v[1]), pack2(v[2], v[3])};
 }
 
+// The per-column (bias, int8 weight scales) and per-row (int8 activation scales) operands of a
+// wave's 128 x (16 NT) accumulator block, loaded ONCE before its stores: read inside the store
+// loop, hipcc may not move them above an earlier store to `out` (possible alias), and every
+// 16-byte store then waits (vmcnt(0)) for its own completion before the next operand load -- 32
+// serialised store round trips per wave in the 128x128 form.
+template <bool I8, int NT>
+struct EpiCols {
+  u32x2_t bw[NT];
+  f32x4_t sw[I8 ? NT : 1];
+  float sx[I8 ? 8 : 1];
+};
+template <bool I8, int NT>
+__device__ __forceinline__ void epi_cols_load(EpiCols<I8, NT>& c, const EpiArgs& e, int M, int N, int mrow0,
+                                              int ncol0, int lane) {
+  const int g = lane >> 4, fr = lane & 15;
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    const int n = min(ncol0 + j * 16 + g * 4, N - 4);
+    c.bw[j] = *(const u32x2_t*)(e.bias + n);
+    if constexpr (I8) c.sw[j] = *(const f32x4_t*)(e.sw + n);
+  }
+  if constexpr (I8) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) c.sx[i] = e.sx[min(mrow0 + i * 16 + fr, M - 1)];
+  }
+}
+// epi_pre on preloaded operands: accumulator tile (i, j) of the block, the same arithmetic
+template <int EPI, bool I8, int NT>
+__device__ __forceinline__ u32x2_t epi_pre_c(const EpiCols<I8, NT>& c, int i, int j,
+                                             const typename MfmaOp<I8>::acc& a) {
+  const u32x2_t bw = c.bw[j];
+  const float b4[4] = {lo_f(bw.x), hi_f(bw.x), lo_f(bw.y), hi_f(bw.y)};
+  float v[4];
+  if constexpr (I8) {
+    const float sx = c.sx[i];
+    const f32x4_t sw = c.sw[j];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = rbf(__builtin_fmaf((float)a[k], sx * sw[k], b4[k]));
+  } else {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = rbf(a[k] + b4[k]);
+  }
+  if constexpr (EPI == EPI_GELU) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = gelu_tanh_f(v[k]);
+  }
+  return u32x2_t{pack2(v[0], v[1]), pack2(v[2], v[3])};
+}
+
 // Post-swap part: 8 consecutive bf16 columns n..n+7 of row m (16-byte aligned, host-checked).
 template <int EPI>
 __device__ __forceinline__ void epi_store8(const EpiArgs& e, int m, int n, u32x4_t v) {
@@ -372,8 +421,9 @@ constexpr int kRingNT = QIE_RING_NT;
 #ifndef QIE_W4_DMA  // gemm_w4: where the 16 DMA pieces of tile k+2 go in stage B (see the kernel)
 #define QIE_W4_DMA 1
 #endif
-#ifndef QIE_GEMM_W4  // big plain / GELU / residual shapes: 1 gemm_w4_kernel (4 waves of 128x128, LDS-DMA), 2 gemm_w4s_kernel (VGPR-staged)
-#define QIE_GEMM_W4 0
+#ifndef QIE_GEMM_W4  // big plain / GELU / residual / QKV shapes: 1 gemm_w4_kernel (4 waves of 128x128, LDS-DMA),
+                     // 2 gemm_w4s_kernel (VGPR-staged), 3 gemm_w4l_kernel (the library's schedule), 0 gemm_pp
+#define QIE_GEMM_W4 3
 #endif
 #ifndef QIE_GEMM_PP  // 1: gemm_pp_kernel for the big shapes (+14 % over gemm_ring in A/B); 0: gemm_ring
 #define QIE_GEMM_PP 1
@@ -476,6 +526,8 @@ __device__ __forceinline__ void ring_epilogue(typename MfmaOp<I8>::acc (&acc)[8]
     }
     return;
   }
+  EpiCols<I8, NT> cols;
+  epi_cols_load<I8, NT>(cols, e, M, N, mrow0, ncol0, lane);
   constexpr bool QKV = EPI == EPI_QKV || EPI == EPI_QKV_NR;
   if constexpr (QKV && NT == 4) {
     if (EPI == EPI_QKV_NR || e.head_dim == 128) {
@@ -488,8 +540,8 @@ __device__ __forceinline__ void ring_epilogue(typename MfmaOp<I8>::acc (&acc)[8]
       auto cols8 = [&](int i, int jp) -> u32x4_t {
         const int mc = min(mrow0 + i * 16 + fr, M - 1);
         const int nb = ncol0 + jp * 32;
-        u32x2_t a = epi_pre<EPI, I8>(e, mc, nb + g * 4, acc[i][2 * jp]);
-        u32x2_t b = epi_pre<EPI, I8>(e, mc, nb + 16 + g * 4, acc[i][2 * jp + 1]);
+        u32x2_t a = epi_pre_c<EPI, I8, NT>(cols, i, 2 * jp, acc[i][2 * jp]);
+        u32x2_t b = epi_pre_c<EPI, I8, NT>(cols, i, 2 * jp + 1, acc[i][2 * jp + 1]);
         const auto sx = __builtin_amdgcn_permlane16_swap(a.x, b.x, false, false);
         const auto sy = __builtin_amdgcn_permlane16_swap(a.y, b.y, false, false);
         return u32x4_t{sx[0], sy[0], sx[1], sy[1]};
@@ -622,8 +674,8 @@ __device__ __forceinline__ void ring_epilogue(typename MfmaOp<I8>::acc (&acc)[8]
 #pragma unroll
         for (int jp = 0; jp < 2; ++jp) {
           const int nb = ncol0 + jp * 32;
-          u32x2_t a = epi_pre<EPI, I8>(e, mc, min(nb + g * 4, N - 4), acc[i][2 * jp]);
-          u32x2_t b = epi_pre<EPI, I8>(e, mc, min(nb + 16 + g * 4, N - 4), acc[i][2 * jp + 1]);
+          u32x2_t a = epi_pre_c<EPI, I8, NT>(cols, i, 2 * jp, acc[i][2 * jp]);
+          u32x2_t b = epi_pre_c<EPI, I8, NT>(cols, i, 2 * jp + 1, acc[i][2 * jp + 1]);
           const auto sx = __builtin_amdgcn_permlane16_swap(a.x, b.x, false, false);
           const auto sy = __builtin_amdgcn_permlane16_swap(a.y, b.y, false, false);
           const uint32_t vv[4] = {sx[0], sy[0], sx[1], sy[1]};
@@ -665,8 +717,8 @@ __device__ __forceinline__ void ring_epilogue(typename MfmaOp<I8>::acc (&acc)[8]
 #pragma unroll
         for (int jp = 0; jp < 2; ++jp) {
           const int nb = ncol0 + jp * 32;
-          u32x2_t a = epi_pre<EPI, I8>(e, mc, min(nb + g * 4, N - 4), acc[i][2 * jp]);
-          u32x2_t b = epi_pre<EPI, I8>(e, mc, min(nb + 16 + g * 4, N - 4), acc[i][2 * jp + 1]);
+          u32x2_t a = epi_pre_c<EPI, I8, NT>(cols, i, 2 * jp, acc[i][2 * jp]);
+          u32x2_t b = epi_pre_c<EPI, I8, NT>(cols, i, 2 * jp + 1, acc[i][2 * jp + 1]);
           const auto sx = __builtin_amdgcn_permlane16_swap(a.x, b.x, false, false);
           const auto sy = __builtin_amdgcn_permlane16_swap(a.y, b.y, false, false);
           const uint32_t vv[4] = {sx[0], sy[0], sx[1], sy[1]};
@@ -691,8 +743,8 @@ __device__ __forceinline__ void ring_epilogue(typename MfmaOp<I8>::acc (&acc)[8]
 #pragma unroll
       for (int jp = 0; jp < NT / 2; ++jp) {
         const int nb = ncol0 + jp * 32;
-        u32x2_t a = epi_pre<EPI, I8>(e, mc, min(nb + g * 4, N - 4), acc[i][2 * jp]);
-        u32x2_t b = epi_pre<EPI, I8>(e, mc, min(nb + 16 + g * 4, N - 4), acc[i][2 * jp + 1]);
+        u32x2_t a = epi_pre_c<EPI, I8, NT>(cols, i, 2 * jp, acc[i][2 * jp]);
+        u32x2_t b = epi_pre_c<EPI, I8, NT>(cols, i, 2 * jp + 1, acc[i][2 * jp + 1]);
         const auto sx = __builtin_amdgcn_permlane16_swap(a.x, b.x, false, false);
         const auto sy = __builtin_amdgcn_permlane16_swap(a.y, b.y, false, false);
         const int n = nb + (g & 1) * 16 + (g >> 1) * 8;
@@ -1396,6 +1448,262 @@ __global__ void __launch_bounds__(256, 1)
   ring_epilogue<8, EPI, I8>(acc, e, M, N, m0 + wm * 128, n0 + wn * 128, lane, smem);
 }
 
+// ---------------------------------------------------------------------------------------------
+// gemm_w4l: gemm_w4's tile (4 waves of 128x128, 256 AGPR accumulators) and LDS image (two slots
+// of [X 256 rows | W 256 rows] x 128 B, XOR-swizzled chunks, filled by LDS-DMA) on the schedule of
+// the library's fastest kernel for these shapes (hipBLASLt's MT256x256x64 MI16x16 DirectToLds
+// PGR2 kernel, studied in its disassembly). The difference to gemm_w4 is where the time goes:
+// every fragment of a whole 64-wide K tile is held in VGPRs (2 sets x 16 x 4 = 128 VGPRs), and
+// the k-step 1 fragments are read one per MFMA at the START of the tile, so the tile's LDS slot
+// is free early and the 16 DMA pieces of tile kt+2 spread over the other ~90 MFMAs instead of
+// bursting. Per tile kt (128 MFMAs per wave; set 0 = the k-step 0 fragments, already in flight):
+//   phase A (k-step 0): set 1 read behind MFMAs 0-15 (lgkmcnt(7) before MFMA 0, lgkmcnt(8) before
+//     MFMA 8 retire set 0); at MFMA QB1 `lgkmcnt(0); s_barrier` -- every wave has read all of
+//     tile kt -- then the 8 X pieces of tile kt+2 into tile kt's slot, one per DS1 MFMAs;
+//   phase B (k-step 1, set 1): the 8 W pieces of tile kt+2, one per DS2 MFMAs; at MFMA 64 + QB2
+//     `vmcnt(16); s_barrier` -- this wave's pieces of tile kt+1 (issued a whole tile earlier)
+//     have landed, and after the barrier everyone's -- then set 0 of tile kt+1, one per MFMA.
+// Two barriers per 128 MFMAs. The reads are inline asm with hand-counted lgkmcnt waits (hipcc
+// counts neither them nor the DMA pieces, so it adds no waits of its own in the loop).
+#ifndef QIE_W4L_QB1  // MFMA of phase A after which the slot-free barrier sits
+#define QIE_W4L_QB1 24
+#endif
+#ifndef QIE_W4L_DS1  // MFMAs between the X pieces (phase A)
+#define QIE_W4L_DS1 3
+#endif
+#ifndef QIE_W4L_DS2  // MFMAs between the W pieces (phase B)
+#define QIE_W4L_DS2 5
+#endif
+#ifndef QIE_W4L_QB2  // MFMA of phase B after which the tile-landed barrier sits (then 16 reads)
+#define QIE_W4L_QB2 48
+#endif
+#ifndef QIE_W4L_PRIO  // s_setprio 3 over the MFMA runs, 0 before each barrier (the library's form)
+#define QIE_W4L_PRIO 1
+#endif
+
+template <int B, int E, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
+  }
+}
+
+#ifndef QIE_W4L_XAUX  // cache bits of the X / W pieces: 0 none, 1 sc0 sc1, 2 nt, 3 sc1, 4 sc0
+#define QIE_W4L_XAUX 0
+#endif
+#ifndef QIE_W4L_WAUX
+#define QIE_W4L_WAUX 0
+#endif
+#ifndef QIE_W4L_ABL  // timing ablations (wrong results): 1 no DMA in the loop, 2 no vmcnt wait, 4 no W DMA, 8 no X DMA
+#define QIE_W4L_ABL 0
+#endif
+template <int AUX>
+__device__ __forceinline__ void w4l_dma(const i32x4_t& r, const char QIE_LDS* dst, uint32_t voff, int soff) {
+  const int lds = __builtin_amdgcn_readfirstlane((int)(uint32_t)(uintptr_t)dst);
+#define QIE_W4L_DMA_ASM(BITS)                                                           \
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, %3 offen" BITS " lds" \
+               :                                                                        \
+               : "v"(voff), "s"(r), "s"(lds), "s"(soff)                                 \
+               : "memory", "m0")
+  if constexpr (AUX == 1) QIE_W4L_DMA_ASM(" sc0 sc1");
+  else if constexpr (AUX == 2) QIE_W4L_DMA_ASM(" nt");
+  else if constexpr (AUX == 3) QIE_W4L_DMA_ASM(" sc1");
+  else if constexpr (AUX == 4) QIE_W4L_DMA_ASM(" sc0");
+  else QIE_W4L_DMA_ASM("");
+#undef QIE_W4L_DMA_ASM
+}
+
+#ifndef QIE_W4L_UNIFORM  // 1: the 16 pieces evenly over MFMAs QB1+1 .. 64+QB2-2 (QIE_W4L_ALT: X, W alternating)
+#define QIE_W4L_UNIFORM 1
+#endif
+#ifndef QIE_W4L_ALT
+#define QIE_W4L_ALT 0
+#endif
+// piece k (0..15) goes after MFMA g_k = QB1 + 1 + k * span / 16 of the tile's 128
+__host__ __device__ constexpr int w4l_piece(int g) {
+  constexpr int first = QIE_W4L_QB1 + 1, span = 64 + QIE_W4L_QB2 - 1 - first;
+  for (int k = 0; k < 16; ++k)
+    if (first + k * span / 16 == g) return k;
+  return -1;
+}
+
+template <int OFF, class FR>
+__device__ __forceinline__ void w4l_read(FR& f, uint32_t addr) {
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(f) : "v"(addr), "i"(OFF));
+}
+
+template <int EPI, bool I8>
+__global__ void __launch_bounds__(256, 1)
+    gemm_w4l_kernel(const char* __restrict__ X, int64_t ldx_b, const char* __restrict__ W, int64_t ldw_b,
+                    int M, int N, int K_bytes, EpiArgs e) {
+  using frag = typename MfmaOp<I8>::frag;
+  using accT = typename MfmaOp<I8>::acc;
+  constexpr int NWAVE = 4, PPO = 8;  // PPO: DMA pieces per wave per operand tile
+  constexpr int kSlot = 2 * kPPTile;  // 64 KiB: X tile then W tile
+  static_assert(QIE_W4L_QB1 >= 16 && (QIE_W4L_UNIFORM || QIE_W4L_QB1 + 1 + 7 * QIE_W4L_DS1 < 64), "phase A placement");
+  static_assert(QIE_W4L_UNIFORM || 1 + 7 * QIE_W4L_DS2 < QIE_W4L_QB2, "phase B placement");
+  static_assert(QIE_W4L_QB2 + 16 <= 64, "phase B reads");
+  __shared__ __attribute__((aligned(16))) char smem_raw[2 * kSlot];
+  char QIE_LDS* smem = (char QIE_LDS*)smem_raw;
+
+  const int tiles_m = (M + 255) >> 8, tiles_n = (N + 255) >> 8;
+  const int nwg = tiles_m * tiles_n;
+  const int wgid = xcd_remap(blockIdx.x, nwg);
+  constexpr int GROUP = 8;
+  const int per_group = GROUP * tiles_n;
+  const int first_m = (wgid / per_group) * GROUP;
+  const int gsz = min(tiles_m - first_m, GROUP);
+  const int tm = first_m + (wgid % per_group) % gsz;
+  const int tn = (wgid % per_group) / gsz;
+  const int m0 = tm * 256, n0 = tn * 256;
+
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int m_valid = M - m0, n_valid = N - n0;
+  const int nk = K_bytes / kRowBytes;  // host guarantees nk >= 3
+
+  const int64_t koff = (int64_t)blockIdx.y * K_bytes;  // split-K range (gridDim.y == 1 otherwise)
+  const i32x4_t xr = pp_rsrc(X + (int64_t)m0 * ldx_b + koff, (int)(min(m_valid, 256) * ldx_b - koff));
+  const i32x4_t wr = pp_rsrc(W + (int64_t)n0 * ldw_b + koff, (int)(min(n_valid, 256) * ldw_b - koff));
+  // piece p of an operand tile: rows 8 (wave + 4 p) .. +7, lane -> row + (lane >> 3), swizzled chunk
+  uint32_t xo[PPO], wo[PPO];
+#pragma unroll
+  for (int i = 0; i < PPO; ++i) {
+    const int r = (wave + i * NWAVE) * 8 + (lane >> 3);
+    const int c = swz_chunk(r, lane & 7);
+    xo[i] = (uint32_t)(min(r, m_valid - 1) * ldx_b) + (c << 4);
+    wo[i] = (uint32_t)(min(r, n_valid - 1) * ldw_b) + (c << 4);
+  }
+  auto dmaX = [&](int kt, int p) {
+    w4l_dma<QIE_W4L_XAUX>(xr, smem + (kt & 1) * kSlot + (wave + p * NWAVE) * 1024, xo[p], kt * kRowBytes);
+  };
+  auto dmaW = [&](int kt, int p) {
+    w4l_dma<QIE_W4L_WAUX>(wr, smem + (kt & 1) * kSlot + kPPTile + (wave + p * NWAVE) * 1024, wo[p], kt * kRowBytes);
+  };
+
+  // piece k of the uniform schedule: X pieces 0..7 then W (or alternating with QIE_W4L_ALT)
+  auto dma_piece_k = [&](int kt, int k) {
+    const bool is_x = QIE_W4L_ALT ? (k & 1) == 0 : k < PPO;
+    const int p = QIE_W4L_ALT ? k >> 1 : (k & (PPO - 1));
+    if (is_x) {
+      if constexpr (!(QIE_W4L_ABL & 9)) dmaX(kt, p);
+    } else {
+      if constexpr (!(QIE_W4L_ABL & 5)) dmaW(kt, p);
+    }
+  };
+  // fragment read addresses: fragment r of a set sits 16 rows (2 KiB) after fragment r - 1, and
+  // k-step 1's chunk is k-step 0's ^ 4; the slot bit (64 KiB) is toggled per tile
+  const int fr = lane & 15;
+  const int sw = (fr >> 1) & 7;
+  const uint32_t lds0 = (uint32_t)(uintptr_t)smem;
+  const uint32_t c0 = (uint32_t)(((lane >> 4) ^ sw) << 4), c1 = (uint32_t)(((4 + (lane >> 4)) ^ sw) << 4);
+  uint32_t xa0 = lds0 + (wm * 128 + fr) * kRowBytes + c0;
+  uint32_t wa0 = lds0 + kPPTile + (wn * 128 + fr) * kRowBytes + c0;
+  uint32_t xa1 = (lds0 + kSlot + (wm * 128 + fr) * kRowBytes + c1);           // slot 1: toggled at tile 0
+  uint32_t wa1 = (lds0 + kSlot + kPPTile + (wn * 128 + fr) * kRowBytes + c1);
+
+  accT acc[8][8];
+  frag wf[2][8], af[2][8];
+
+  // the 16 reads of one set in the order the MFMAs consume them: W0, X0, W1..W7, X1..X7
+  auto rd = [&](auto set_t, auto r_t) {
+    constexpr int S = decltype(set_t)::value, R = decltype(r_t)::value;
+    const uint32_t xa = S ? xa1 : xa0, wa = S ? wa1 : wa0;
+    if constexpr (R == 0) w4l_read<0>(wf[S][0], wa);
+    else if constexpr (R == 1) w4l_read<0>(af[S][0], xa);
+    else if constexpr (R < 9) w4l_read<2048 * (R - 1)>(wf[S][R - 1], wa);
+    else w4l_read<2048 * (R - 8)>(af[S][R - 8], xa);
+  };
+  auto prio = [&](auto p_t) {
+    if constexpr (QIE_W4L_PRIO) __builtin_amdgcn_s_setprio(decltype(p_t)::value);
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I3 = std::integral_constant<int, 3>;
+
+  // one K tile. INIT: first tile (accumulators start at 0); DMA: stage tile kt+2; NEXT: read set 0
+  // of tile kt+1 at the end
+  auto tile = [&](auto init_t, auto dma_t, auto next_t, int kt) {
+    constexpr bool INIT = decltype(init_t)::value, DMA = decltype(dma_t)::value, NEXT = decltype(next_t)::value;
+    xa1 ^= (uint32_t)kSlot;
+    wa1 ^= (uint32_t)kSlot;
+    // ---- phase A: k-step 0 on set 0
+    static_for<0, 64>([&](auto q_t) {
+      constexpr int q = decltype(q_t)::value;
+      constexpr int i = q >> 3, j = q & 7;
+      if constexpr (q == 0) asm volatile("s_waitcnt lgkmcnt(7)" ::: "memory");
+      if constexpr (q == 8) asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
+      if constexpr (INIT) Mma4<I8>::init(acc[i][j], wf[0][j], af[0][i]);
+      else Mma4<I8>::acc(acc[i][j], wf[0][j], af[0][i]);
+      if constexpr (q < 16) rd(I1{}, q_t);
+      if constexpr (q == QIE_W4L_QB1) {
+        prio(I0{});
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        prio(I3{});
+      }
+      if constexpr (DMA && QIE_W4L_UNIFORM) {
+        constexpr int k = w4l_piece(q);
+        if constexpr (k >= 0) dma_piece_k(kt + 2, k);
+      } else if constexpr (DMA && !(QIE_W4L_ABL & 9) && q > QIE_W4L_QB1 && (q - QIE_W4L_QB1 - 1) % QIE_W4L_DS1 == 0 &&
+                           (q - QIE_W4L_QB1 - 1) / QIE_W4L_DS1 < PPO)
+        dmaX(kt + 2, (q - QIE_W4L_QB1 - 1) / QIE_W4L_DS1);
+    });
+    // ---- phase B: k-step 1 on set 1
+    if constexpr (NEXT) {
+      xa0 ^= (uint32_t)kSlot;
+      wa0 ^= (uint32_t)kSlot;
+    }
+    static_for<0, 64>([&](auto q_t) {
+      constexpr int q = decltype(q_t)::value;
+      constexpr int i = q >> 3, j = q & 7;
+      Mma4<I8>::acc(acc[i][j], wf[1][j], af[1][i]);
+      if constexpr (DMA && QIE_W4L_UNIFORM) {
+        constexpr int k = w4l_piece(64 + q);
+        if constexpr (k >= 0) dma_piece_k(kt + 2, k);
+      } else if constexpr (DMA && !(QIE_W4L_ABL & 5) && q >= 1 && (q - 1) % QIE_W4L_DS2 == 0 &&
+                           (q - 1) / QIE_W4L_DS2 < PPO)
+        dmaW(kt + 2, (q - 1) / QIE_W4L_DS2);
+      if constexpr (NEXT && q == QIE_W4L_QB2) {
+        prio(I0{});
+        if constexpr (QIE_W4L_ABL & 15) asm volatile("s_barrier" ::: "memory");
+        else if constexpr (DMA) asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+        prio(I3{});
+      }
+      if constexpr (NEXT && q >= QIE_W4L_QB2 && q < QIE_W4L_QB2 + 16) rd(I0{}, std::integral_constant<int, q - QIE_W4L_QB2>{});
+    });
+    prio(I0{});
+  };
+  using T = std::true_type;
+  using F = std::false_type;
+
+  // prologue: tiles 0 and 1 in flight, tile 0 landed everywhere, set 0 of tile 0 read
+#pragma unroll
+  for (int p = 0; p < PPO; ++p) dmaX(0, p);
+#pragma unroll
+  for (int p = 0; p < PPO; ++p) dmaW(0, p);
+#pragma unroll
+  for (int p = 0; p < PPO; ++p) dmaX(1, p);
+#pragma unroll
+  for (int p = 0; p < PPO; ++p) dmaW(1, p);
+  asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
+  static_for<0, 16>([&](auto r_t) { rd(I0{}, r_t); });
+  prio(I3{});
+
+  tile(T{}, T{}, T{}, 0);
+  int kt = 1;
+  for (; kt < nk - 2; ++kt) tile(F{}, T{}, T{}, kt);
+  tile(F{}, F{}, T{}, kt);      // nk-2: nothing left to stage, reads tile nk-1
+  tile(F{}, F{}, F{}, kt + 1);  // nk-1
+  asm volatile("s_barrier" ::: "memory");  // no wave's epilogue LDS use overlaps another's reads
+
+  if (QIE_W4L_ABL & 16) {  // timing ablation: the epilogue only for a never-seen ldo (no stores)
+    if (e.ldo != -12345) return;
+  }
+  ring_epilogue<8, EPI, I8>(acc, e, M, N, m0 + wm * 128, n0 + wn * 128, lane, smem);
+}
+
 template <int EPI, bool I8>
 int launch_gemm(const void* x, int64_t ldx, const void* w, int64_t ldw, int M, int N, int K,
                 const EpiArgs& e, hipStream_t s) {
@@ -1412,7 +1720,10 @@ int launch_gemm(const void* x, int64_t ldx, const void* w, int64_t ldw, int M, i
                     (EPI != EPI_GATE_RES || (((uintptr_t)e.gate % 16) == 0 && e.gate_bstride % 8 == 0)) &&
                     (EPI != EPI_QKV || e.head_dim % 8 == 0);
   if (wide && M >= 256 && N >= 256 && big_tiles >= 160 && kb >= (kRingD + 2) * k4RowBytes) {
-    if constexpr (QIE_GEMM_W4 == 2 && EPI != EPI_QKV_NR)
+    if constexpr (QIE_GEMM_W4 == 3 && EPI != EPI_QKV_NR)
+      gemm_w4l_kernel<EPI, I8><<<(int)big_tiles, 256, 0, s>>>((const char*)x, ldx_b, (const char*)w, ldw_b, M, N,
+                                                             kb, e);
+    else if constexpr (QIE_GEMM_W4 == 2 && EPI != EPI_QKV_NR)
       gemm_w4s_kernel<EPI, I8><<<(int)big_tiles, 256, 0, s>>>((const char*)x, ldx_b, (const char*)w, ldw_b, M, N,
                                                              kb, e);
     else if constexpr (QIE_GEMM_W4 == 1 && EPI != EPI_QKV_NR)

@@ -38,11 +38,12 @@ def main():
     what = sys.argv[1]
     # "lib.so@log2q": the attention entry for a q plane pre-multiplied by scale*log2(e)
     args = [a.split("@") for a in sys.argv[2:]]
-    paths = [a[0] for a in args if a[0].endswith(".so")]
-    modes = [a[1] if len(a) > 1 else "" for a in args if a[0].endswith(".so")]
-    rest = [a[0] for a in args if not a[0].endswith(".so")]
+    # "torch": the library reference (hipBLASLt through F.linear) for the gemm shapes
+    paths = [a[0] for a in args if a[0].endswith(".so") or a[0] == "torch"]
+    modes = [a[1] if len(a) > 1 else "" for a in args if a[0].endswith(".so") or a[0] == "torch"]
+    rest = [a[0] for a in args if not (a[0].endswith(".so") or a[0] == "torch")]
     rounds = int(rest[0]) if rest else 10
-    libs = [load(p) for p in paths]
+    libs = [load(p) if p != "torch" else None for p in paths]
     dev = torch.device("cuda:0")
     st = torch.cuda.current_stream().cuda_stream
     if what in ("attention", "attention_nosplit"):
@@ -150,6 +151,9 @@ def main():
         flops = 2.0 * M * N * K
 
         def run(i):
+            if libs[i] is None:
+                torch.mm(x, w.t(), out=outs[i])
+                return
             rc = libs[i].qie_linear_bf16(x.data_ptr(), K, w.data_ptr(), b.data_ptr(), outs[i].data_ptr(), N,
                                          M, N, K, 0, st)
             assert rc == 0, rc

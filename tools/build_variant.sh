@@ -6,11 +6,13 @@ cd "$(dirname "$0")/.."
 NAME=$1; shift
 OUT=tools/ab_build/$NAME
 mkdir -p $OUT
+pids=()
 for f in qwen_image_edit_streamdiffusion_amd/csrc/*.hip; do
-  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-function "$@" \
+  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-function -Wno-inline-asm "$@" \
     -c $f -o $OUT/$(basename $f .hip).o &
+  pids+=($!)
 done
-wait
+for p in "${pids[@]}"; do wait $p || { echo "build of $NAME failed" >&2; exit 1; }; done
 /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o tools/ab_build/$NAME.so $OUT/*.o
 rm -rf $OUT
 echo tools/ab_build/$NAME.so
