@@ -504,15 +504,21 @@ struct Mma4<true> {
 template <int NT, int EPI, bool I8>
 __device__ __forceinline__ void ring_epilogue(typename MfmaOp<I8>::acc (&acc)[8][NT], const EpiArgs& e, int M,
                                               int N, int mrow0, int ncol0, int lane, char QIE_LDS* smem) {
-  // MFMA D -> VALU read hazard for the last row of accumulators (asm is not padded by hipcc)
-  if constexpr (NT == 8)
-    asm volatile("s_nop 15\n\ts_nop 7"
-                 : "+a"(acc[7][0]), "+a"(acc[7][1]), "+a"(acc[7][2]), "+a"(acc[7][3]), "+a"(acc[7][4]),
-                   "+a"(acc[7][5]), "+a"(acc[7][NT - 2]), "+a"(acc[7][NT - 1]));
-  else
-    asm volatile("s_nop 15\n\ts_nop 7"
-                 : "+a"(acc[7][0]), "+a"(acc[7][1]), "+a"(acc[7][2]), "+a"(acc[7][3]), "+a"(acc[6][0]),
-                   "+a"(acc[6][1]), "+a"(acc[6][2]), "+a"(acc[6][NT - 1]));
+  // MFMA D -> VALU read hazard (the MFMAs are inline asm, so hipcc pads nothing): 23 wait states
+  // behind the last MFMA, then EVERY accumulator is redefined by an (empty) asm statement, so no
+  // read of one -- an epilogue read, or a copy the register allocator makes on its own -- can be
+  // placed above the nops, inside the tail of the MFMA stream, right behind the asm MFMA that
+  // wrote the register (hipcc did exactly that for the register-heavy QKV + norm + RoPE form:
+  // stale reads no hazard pass knew about)
+  asm volatile("s_nop 15\n\ts_nop 7" ::: "memory");
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    if constexpr (NT == 8)
+      asm volatile("" : "+a"(acc[i][0]), "+a"(acc[i][1]), "+a"(acc[i][2]), "+a"(acc[i][3]), "+a"(acc[i][4]),
+                   "+a"(acc[i][5]), "+a"(acc[i][6]), "+a"(acc[i][7]));
+    else
+      asm volatile("" : "+a"(acc[i][0]), "+a"(acc[i][1]), "+a"(acc[i][2]), "+a"(acc[i][NT - 1]));
+  }
   const int g = lane >> 4, fr = lane & 15;
   if constexpr (EPI == EPI_PARTIAL) {  // raw fp32 / int32 partial sums of split blockIdx.y
 #pragma unroll
@@ -529,12 +535,14 @@ __device__ __forceinline__ void ring_epilogue(typename MfmaOp<I8>::acc (&acc)[8]
   EpiCols<I8, NT> cols;
   epi_cols_load<I8, NT>(cols, e, M, N, mrow0, ncol0, lane);
   constexpr bool QKV = EPI == EPI_QKV || EPI == EPI_QKV_NR;
-  if constexpr (QKV && NT == 4) {
+  if constexpr (QKV && (NT == 4 || NT == 8)) {
+    // NT == 4: the wave's 64 columns are one half of a head (its partner wave holds the other);
+    // NT == 8: the wave's 128 columns are one whole head
     if (EPI == EPI_QKV_NR || e.head_dim == 128) {
       const int hd = e.heads * 128;
       const int which = ncol0 / hd;
       const int h = (ncol0 - which * hd) >> 7;
-      const int dbase = ncol0 & 127;               // 0 or 64
+      const int dbase = ncol0 & 127;               // 0 or 64 (NT == 4), 0 (NT == 8)
       const int dl = (g & 1) * 16 + (g >> 1) * 8;  // the lane's column offset inside a 32-col pair
       // the lane's 8 consecutive bf16 of row i, column pair jp (bias added, rounded)
       auto cols8 = [&](int i, int jp) -> u32x4_t {
@@ -554,14 +562,12 @@ __device__ __forceinline__ void ring_epilogue(typename MfmaOp<I8>::acc (&acc)[8]
       bool done = false;
       if constexpr (EPI == EPI_QKV_NR) {
         if (which < 2) {
-          // pass 1: sum of squares of the rounded values over the wave's 64 columns of each row,
-          // plus the partner wave's 64 (the other half of the head) through LDS
-          float ss[8];
-#pragma unroll
-          for (int i = 0; i < 8; ++i) {
+          // pass 1: sum of squares of the rounded values over each 64-column half of the head
+          // (the same order in both forms), the two halves added last
+          auto half_ss = [&](int i, int hh) {
             float t = 0.f;
 #pragma unroll
-            for (int jp = 0; jp < 2; ++jp) {
+            for (int jp = 2 * hh; jp < 2 * hh + 2; ++jp) {
               const u32x4_t v = cols8(i, jp);
               const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
@@ -572,22 +578,30 @@ __device__ __forceinline__ void ring_epilogue(typename MfmaOp<I8>::acc (&acc)[8]
             }
             t += __shfl_xor(t, 16, 64);
             t += __shfl_xor(t, 32, 64);
-            ss[i] = t;
-          }
-          const int wave = threadIdx.x >> 6;
-          float QIE_LDS* red = (float QIE_LDS*)smem;
-          if (g == 0) {
+            return t;
+          };
+          float ss[8];
+          if constexpr (NT == 8) {
 #pragma unroll
-            for (int i = 0; i < 8; ++i) red[wave * 128 + i * 16 + fr] = ss[i];
-          }
-          __syncthreads();
+            for (int i = 0; i < 8; ++i) ss[i] = rsqrtf((half_ss(i, 0) + half_ss(i, 1)) * (1.0f / 128.0f) + e.eps);
+          } else {  // the partner wave's half through LDS
 #pragma unroll
-          for (int i = 0; i < 8; ++i) ss[i] = rsqrtf((ss[i] + red[(wave ^ 1) * 128 + i * 16 + fr]) * (1.0f / 128.0f) + e.eps);
+            for (int i = 0; i < 8; ++i) ss[i] = half_ss(i, 0);
+            const int wave = threadIdx.x >> 6;
+            float QIE_LDS* red = (float QIE_LDS*)smem;
+            if (g == 0) {
+#pragma unroll
+              for (int i = 0; i < 8; ++i) red[wave * 128 + i * 16 + fr] = ss[i];
+            }
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < 8; ++i) ss[i] = rsqrtf((ss[i] + red[(wave ^ 1) * 128 + i * 16 + fr]) * (1.0f / 128.0f) + e.eps);
+          }
           const bf16_t* nw = which == 0 ? e.nq : e.nk;
           const float osc = which == 0 ? e.qscale : 1.0f;
           // pass 2: recompute the rounded values, RMSNorm (two bf16 roundings) and rotate
 #pragma unroll
-          for (int jp = 0; jp < 2; ++jp) {
+          for (int jp = 0; jp < NT / 2; ++jp) {
             const int d0 = dbase + jp * 32 + dl;
             const u32x4_t ww = *(const u32x4_t*)(nw + d0);
             const uint32_t wv[4] = {ww.x, ww.y, ww.z, ww.w};
@@ -638,11 +652,13 @@ __device__ __forceinline__ void ring_epilogue(typename MfmaOp<I8>::acc (&acc)[8]
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           const int m = mrow0 + i * 16 + fr;
-          const u32x4_t v0 = cols8(i, 0), v1 = cols8(i, 1);
+          u32x4_t v[NT / 2];
+#pragma unroll
+          for (int jp = 0; jp < NT / 2; ++jp) v[jp] = cols8(i, jp);
           if (m < M) {
             bf16_t* row = row_ptr(m);
-            *(u32x4_t*)row = v0;
-            *(u32x4_t*)(row + 32) = v1;
+#pragma unroll
+            for (int jp = 0; jp < NT / 2; ++jp) *(u32x4_t*)(row + 32 * jp) = v[jp];
           }
         }
       }
@@ -1720,7 +1736,7 @@ int launch_gemm(const void* x, int64_t ldx, const void* w, int64_t ldw, int M, i
                     (EPI != EPI_GATE_RES || (((uintptr_t)e.gate % 16) == 0 && e.gate_bstride % 8 == 0)) &&
                     (EPI != EPI_QKV || e.head_dim % 8 == 0);
   if (wide && M >= 256 && N >= 256 && big_tiles >= 160 && kb >= (kRingD + 2) * k4RowBytes) {
-    if constexpr (QIE_GEMM_W4 == 3 && EPI != EPI_QKV_NR)
+    if constexpr (QIE_GEMM_W4 == 3)
       gemm_w4l_kernel<EPI, I8><<<(int)big_tiles, 256, 0, s>>>((const char*)x, ldx_b, (const char*)w, ldw_b, M, N,
                                                              kb, e);
     else if constexpr (QIE_GEMM_W4 == 2 && EPI != EPI_QKV_NR)
@@ -1857,8 +1873,13 @@ int launch_qkv_norm_rope(const void* x, int64_t ldx, const void* w, int M, int K
     e.rsin = sin_tab;
     e.eps = eps;
     e.qscale = q_scale;
-    gemm_pp_kernel<EPI_QKV_NR, I8><<<(int)big_tiles, 512, 0, s>>>((const char*)x, ldx * eb, (const char*)w,
-                                                                 (int64_t)K * eb, M, N, K * eb, e);
+    // both kernels compute every row bit for bit alike (same K order, same epilogue sums)
+    if (QIE_GEMM_W4 == 3 && M >= 256 && big_tiles >= 160)
+      gemm_w4l_kernel<EPI_QKV_NR, I8><<<(int)big_tiles, 256, 0, s>>>((const char*)x, ldx * eb, (const char*)w,
+                                                                    (int64_t)K * eb, M, N, K * eb, e);
+    else
+      gemm_pp_kernel<EPI_QKV_NR, I8><<<(int)big_tiles, 512, 0, s>>>((const char*)x, ldx * eb, (const char*)w,
+                                                                   (int64_t)K * eb, M, N, K * eb, e);
     return qie_last_error();
   }
   const int rc = launch_gemm<EPI_QKV, I8>(x, ldx, w, K, M, N, K, e, s);
