@@ -599,6 +599,50 @@ __device__ __forceinline__ void ring_epilogue(typename MfmaOp<I8>::acc (&acc)[8]
           }
           const bf16_t* nw = which == 0 ? e.nq : e.nk;
           const float osc = which == 0 ? e.qscale : 1.0f;
+          if constexpr (NT == 8) {
+            // the work-group's 256 RoPE rows (cos | sin, 512 B of fp32 each) staged into the free
+            // LDS slots in one round trip by LDS-DMA (32 KiB pieces per wave), chunks XOR-swizzled by
+            // the row so the 16 rows of a ds_read_b128 lane group hit 16 different banks; then
+            // pass 2 reads them from LDS -- instead of 8 row-group round trips to L2 per wave, each
+            // held behind the previous group's stores (possible alias with the qkv buffer)
+            const int m0w = mrow0 & ~255, wave = threadIdx.x >> 6;
+#pragma unroll 1
+            for (int p = 0; p < 32; ++p) {
+              const int P = wave * 32 + p, r = 2 * P + (lane >> 5), q = lane & 31;
+              const int sl = min(m0w + r, M - 1) % e.rows_per_batch;
+              const float* src = (q < 16 ? e.rcos : e.rsin) + (int64_t)sl * 64 + (((q & 15) ^ (r & 15)) << 2);
+              __builtin_amdgcn_global_load_lds((const void*)src, (QIE_LDS void*)(smem + P * 1024), 16, 0, 0);
+            }
+            u32x4_t wwv[4];
+#pragma unroll
+            for (int jp = 0; jp < 4; ++jp) wwv[jp] = *(const u32x4_t*)(nw + jp * 32 + dl);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            const int rl0 = (mrow0 & 255) + fr;  // the lane's row in the work-group tile, row group 0
+#pragma unroll
+            for (int jp = 0; jp < 4; ++jp) {
+              const int d0 = jp * 32 + dl;
+              const uint32_t wv[4] = {wwv[jp].x, wwv[jp].y, wwv[jp].z, wwv[jp].w};
+#pragma unroll
+              for (int i = 0; i < 8; ++i) {
+                const int m = mrow0 + i * 16 + fr, rl = rl0 + i * 16;
+                const char QIE_LDS* rrow = smem + rl * 512 + (((d0 >> 3) ^ (rl & 15)) << 4);
+                const f32x4_t cs = *(const f32x4_t QIE_LDS*)rrow;
+                const f32x4_t sn = *(const f32x4_t QIE_LDS*)(rrow + 256);
+                const u32x4_t v = cols8(i, jp);
+                const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+                uint32_t o[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                  const float x0 = rbf(rbf(lo_f(w4[k]) * ss[i]) * lo_f(wv[k]));
+                  const float x1 = rbf(rbf(hi_f(w4[k]) * ss[i]) * hi_f(wv[k]));
+                  o[k] = pack2((x0 * cs[k] - x1 * sn[k]) * osc, (x0 * sn[k] + x1 * cs[k]) * osc);
+                }
+                if (m < M) *(u32x4_t*)(row_ptr(m) + jp * 32) = u32x4_t{o[0], o[1], o[2], o[3]};
+              }
+            }
+            return;
+          }
           // pass 2: recompute the rounded values, RMSNorm (two bf16 roundings) and rotate
 #pragma unroll
           for (int jp = 0; jp < NT / 2; ++jp) {
