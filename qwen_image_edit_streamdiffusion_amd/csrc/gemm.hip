@@ -22,6 +22,7 @@
 // Common: MFMA 16x16x32 bf16 (or 16x16x64 i8) with the WEIGHT tile as the A operand and the
 // activation tile as B, so each lane owns 4 consecutive output columns of one row; XCD-aware
 // bijective block remap + grouped tile order so the 32 CUs of one XCD share L2-resident tiles.
+#include <algorithm>
 #include <type_traits>
 
 #include "qie_common.h"
@@ -423,7 +424,7 @@ constexpr int kRingNT = QIE_RING_NT;
 #endif
 #ifndef QIE_GEMM_W4  // big plain / GELU / residual / QKV shapes: 1 gemm_w4_kernel (4 waves of 128x128, LDS-DMA),
                      // 2 gemm_w4s_kernel (VGPR-staged), 3 gemm_w4l_kernel (the library's schedule), 0 gemm_pp
-#define QIE_GEMM_W4 3
+#define QIE_GEMM_W4 4
 #endif
 #ifndef QIE_GEMM_PP  // 1: gemm_pp_kernel for the big shapes (+14 % over gemm_ring in A/B); 0: gemm_ring
 #define QIE_GEMM_PP 1
@@ -1764,6 +1765,180 @@ __global__ void __launch_bounds__(256, 1)
   ring_epilogue<8, EPI, I8>(acc, e, M, N, m0 + wm * 128, n0 + wn * 128, lane, smem);
 }
 
+// ---------------------------------------------------------------------------------------------
+// gemm_w4p: gemm_w4l as a persistent kernel -- one work-group per CU walks the output tiles
+// b, b + G, b + 2G, ... (the same tile order and XCD placement as one work-group per tile) and
+// runs ONE K-tile pipeline across tile boundaries: the last two K tiles of tile t stage K tiles 0
+// and 1 of tile t+1 and read its first fragment set, so tile t's epilogue (bias / GELU / gated
+// residual and the 128 KiB of stores) runs while the next tile's operands are already landing,
+// and the next tile starts on fragments in registers instead of on a cold prologue.
+// Row / column offsets of the DMA pieces are those of a full 256-row tile; rows past M or N lie
+// past the buffer descriptor's range and read as zeros (never stored). Not for EPI_QKV_NR (its
+// epilogue stages RoPE rows in the LDS the next tile is landing in).
+static int g_cu_count = 0;
+
+template <int EPI, bool I8>
+__global__ void __launch_bounds__(256, 1)
+    gemm_w4p_kernel(const char* __restrict__ X, int64_t ldx_b, const char* __restrict__ W, int64_t ldw_b,
+                    int M, int N, int K_bytes, EpiArgs e) {
+  static_assert(EPI != EPI_QKV_NR && EPI != EPI_PARTIAL, "w4p epilogues");
+  using frag = typename MfmaOp<I8>::frag;
+  using accT = typename MfmaOp<I8>::acc;
+  constexpr int NWAVE = 4, PPO = 8;
+  constexpr int kSlot = 2 * kPPTile;
+  __shared__ __attribute__((aligned(16))) char smem_raw[2 * kSlot];
+  char QIE_LDS* smem = (char QIE_LDS*)smem_raw;
+
+  const int tiles_m = (M + 255) >> 8, tiles_n = (N + 255) >> 8;
+  const int nwg = tiles_m * tiles_n;
+  const int nk = K_bytes / kRowBytes;  // host guarantees nk >= 3
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int wm = wave >> 1, wn = wave & 1;
+
+  struct TileRef {
+    int m0, n0;
+    i32x4_t xr, wr;
+  };
+  auto tile_of = [&](int vb) {
+    const int wgid = xcd_remap(vb, nwg);
+    constexpr int GROUP = 8;
+    const int per_group = GROUP * tiles_n;
+    const int first_m = (wgid / per_group) * GROUP;
+    const int gsz = min(tiles_m - first_m, GROUP);
+    TileRef t;
+    t.m0 = (first_m + (wgid % per_group) % gsz) * 256;
+    t.n0 = ((wgid % per_group) / gsz) * 256;
+    t.xr = pp_rsrc(X + (int64_t)t.m0 * ldx_b, (int)(min(M - t.m0, 256) * ldx_b));
+    t.wr = pp_rsrc(W + (int64_t)t.n0 * ldw_b, (int)(min(N - t.n0, 256) * ldw_b));
+    return t;
+  };
+  uint32_t xo[PPO], wo[PPO];
+#pragma unroll
+  for (int i = 0; i < PPO; ++i) {
+    const int r = (wave + i * NWAVE) * 8 + (lane >> 3);
+    const int c = swz_chunk(r, lane & 7);
+    xo[i] = (uint32_t)(r * ldx_b) + (c << 4);
+    wo[i] = (uint32_t)(r * ldw_b) + (c << 4);
+  }
+  // piece k (0..15) of K tile dkt of tile tr into LDS slot sl: X pieces 0..7, then W
+  auto dma_piece = [&](const TileRef& tr, int sl, int dkt, int k) {
+    if (k < PPO)
+      w4l_dma<QIE_W4L_XAUX>(tr.xr, smem + sl * kSlot + (wave + k * NWAVE) * 1024, xo[k], dkt * kRowBytes);
+    else
+      w4l_dma<QIE_W4L_WAUX>(tr.wr, smem + sl * kSlot + kPPTile + (wave + (k - PPO) * NWAVE) * 1024, wo[k - PPO],
+                            dkt * kRowBytes);
+  };
+
+  const int fr = lane & 15;
+  const int sw = (fr >> 1) & 7;
+  const uint32_t lds0 = (uint32_t)(uintptr_t)smem;
+  const uint32_t c0 = (uint32_t)(((lane >> 4) ^ sw) << 4), c1 = (uint32_t)(((4 + (lane >> 4)) ^ sw) << 4);
+  uint32_t xa0 = lds0 + (wm * 128 + fr) * kRowBytes + c0;
+  uint32_t wa0 = lds0 + kPPTile + (wn * 128 + fr) * kRowBytes + c0;
+  uint32_t xa1 = (lds0 + kSlot + (wm * 128 + fr) * kRowBytes + c1);
+  uint32_t wa1 = (lds0 + kSlot + kPPTile + (wn * 128 + fr) * kRowBytes + c1);
+
+  accT acc[8][8];
+  frag wf[2][8], af[2][8];
+  auto rd = [&](auto set_t, auto r_t) {
+    constexpr int S = decltype(set_t)::value, R = decltype(r_t)::value;
+    const uint32_t xa = S ? xa1 : xa0, wa = S ? wa1 : wa0;
+    if constexpr (R == 0) w4l_read<0>(wf[S][0], wa);
+    else if constexpr (R == 1) w4l_read<0>(af[S][0], xa);
+    else if constexpr (R < 9) w4l_read<2048 * (R - 1)>(wf[S][R - 1], wa);
+    else w4l_read<2048 * (R - 8)>(af[S][R - 8], xa);
+  };
+  auto prio = [&](auto p_t) {
+    if constexpr (QIE_W4L_PRIO) __builtin_amdgcn_s_setprio(decltype(p_t)::value);
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I3 = std::integral_constant<int, 3>;
+
+  // one K tile in slot sl: INIT (first K tile of an output tile), DMA (stage K tile dkt of tile
+  // dsrc into slot sl), NEXT (read set 0 of the following K tile, in slot sl ^ 1)
+  auto ktile = [&](auto init_t, auto dma_t, auto next_t, int sl, const TileRef& dsrc, int dkt) {
+    constexpr bool INIT = decltype(init_t)::value, DMA = decltype(dma_t)::value, NEXT = decltype(next_t)::value;
+    xa1 ^= (uint32_t)kSlot;
+    wa1 ^= (uint32_t)kSlot;
+    static_for<0, 64>([&](auto q_t) {
+      constexpr int q = decltype(q_t)::value;
+      constexpr int i = q >> 3, j = q & 7;
+      if constexpr (q == 0) asm volatile("s_waitcnt lgkmcnt(7)" ::: "memory");
+      if constexpr (q == 8) asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
+      if constexpr (INIT) Mma4<I8>::init(acc[i][j], wf[0][j], af[0][i]);
+      else Mma4<I8>::acc(acc[i][j], wf[0][j], af[0][i]);
+      if constexpr (q < 16) rd(I1{}, q_t);
+      if constexpr (q == QIE_W4L_QB1) {
+        prio(I0{});
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        prio(I3{});
+      }
+      if constexpr (DMA) {
+        constexpr int k = w4l_piece(q);
+        if constexpr (k >= 0) dma_piece(dsrc, sl, dkt, k);
+      }
+    });
+    if constexpr (NEXT) {
+      xa0 ^= (uint32_t)kSlot;
+      wa0 ^= (uint32_t)kSlot;
+    }
+    static_for<0, 64>([&](auto q_t) {
+      constexpr int q = decltype(q_t)::value;
+      constexpr int i = q >> 3, j = q & 7;
+      Mma4<I8>::acc(acc[i][j], wf[1][j], af[1][i]);
+      if constexpr (DMA) {
+        constexpr int k = w4l_piece(64 + q);
+        if constexpr (k >= 0) dma_piece(dsrc, sl, dkt, k);
+      }
+      if constexpr (NEXT && q == QIE_W4L_QB2) {
+        prio(I0{});
+        if constexpr (DMA) asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+        prio(I3{});
+      }
+      if constexpr (NEXT && q >= QIE_W4L_QB2 && q < QIE_W4L_QB2 + 16) rd(I0{}, std::integral_constant<int, q - QIE_W4L_QB2>{});
+    });
+    prio(I0{});
+  };
+  using T = std::true_type;
+  using F = std::false_type;
+
+  int vb = blockIdx.x;
+  TileRef cur = tile_of(vb);
+  // prologue of the first tile: K tiles 0 and 1 in flight, 0 landed everywhere, set 0 read
+#pragma unroll
+  for (int k = 0; k < 16; ++k) dma_piece(cur, 0, 0, k);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) dma_piece(cur, 1, 1, k);
+  asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
+  static_for<0, 16>([&](auto r_t) { rd(I0{}, r_t); });
+  prio(I3{});
+  int g = 0;  // flat K-tile count of this work-group: K tile kt of the current tile is in slot (g + kt) & 1
+  while (true) {
+    const int vbn = vb + (int)gridDim.x;
+    const bool has_next = vbn < nwg;
+    const TileRef nxt = tile_of(has_next ? vbn : vb);
+    // one code path for every tile (the accumulators must not meet at a branch: hipcc then
+    // shuffles all 256 through VGPRs and scratch); the last tile of the work-group re-stages its
+    // own K tiles 0 and 1 as a stand-in "next" tile and drains them before it exits
+    ktile(T{}, T{}, T{}, g & 1, cur, 2);
+    int kt = 1;
+    for (; kt < nk - 2; ++kt) ktile(F{}, T{}, T{}, (g + kt) & 1, cur, kt + 2);
+    ktile(F{}, T{}, T{}, (g + kt) & 1, nxt, 0);      // nk-2: stages the next tile's K tile 0
+    ktile(F{}, T{}, T{}, (g + kt + 1) & 1, nxt, 1);  // nk-1: its K tile 1, reads its set 0
+    ring_epilogue<8, EPI, I8>(acc, e, M, N, cur.m0 + wm * 128, cur.n0 + wn * 128, lane, smem);
+    if (!has_next) {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // no LDS-DMA outlives the work-group
+      break;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // nothing of the epilogue ahead of set 0's count
+    g += nk;
+    vb = vbn;
+    cur = nxt;
+  }
+}
+
 template <int EPI, bool I8>
 int launch_gemm(const void* x, int64_t ldx, const void* w, int64_t ldw, int M, int N, int K,
                 const EpiArgs& e, hipStream_t s) {
@@ -1780,7 +1955,17 @@ int launch_gemm(const void* x, int64_t ldx, const void* w, int64_t ldw, int M, i
                     (EPI != EPI_GATE_RES || (((uintptr_t)e.gate % 16) == 0 && e.gate_bstride % 8 == 0)) &&
                     (EPI != EPI_QKV || e.head_dim % 8 == 0);
   if (wide && M >= 256 && N >= 256 && big_tiles >= 160 && kb >= (kRingD + 2) * k4RowBytes) {
-    if constexpr (QIE_GEMM_W4 == 3)
+    if constexpr (QIE_GEMM_W4 == 4 && EPI != EPI_QKV_NR) {
+      if (g_cu_count == 0) {
+        int dev = 0, cu = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cu <= 0)
+          cu = 256;
+        g_cu_count = cu;
+      }
+      const int grid = (int)std::min<int64_t>(big_tiles, g_cu_count);
+      gemm_w4p_kernel<EPI, I8><<<grid, 256, 0, s>>>((const char*)x, ldx_b, (const char*)w, ldw_b, M, N, kb, e);
+    } else if constexpr (QIE_GEMM_W4 >= 3)
       gemm_w4l_kernel<EPI, I8><<<(int)big_tiles, 256, 0, s>>>((const char*)x, ldx_b, (const char*)w, ldw_b, M, N,
                                                              kb, e);
     else if constexpr (QIE_GEMM_W4 == 2 && EPI != EPI_QKV_NR)
@@ -1918,7 +2103,7 @@ int launch_qkv_norm_rope(const void* x, int64_t ldx, const void* w, int M, int K
     e.eps = eps;
     e.qscale = q_scale;
     // both kernels compute every row bit for bit alike (same K order, same epilogue sums)
-    if (QIE_GEMM_W4 == 3 && M >= 256 && big_tiles >= 160)
+    if (QIE_GEMM_W4 >= 3 && M >= 256 && big_tiles >= 160)
       gemm_w4l_kernel<EPI_QKV_NR, I8><<<(int)big_tiles, 256, 0, s>>>((const char*)x, ldx * eb, (const char*)w,
                                                                     (int64_t)K * eb, M, N, K * eb, e);
     else

@@ -43,6 +43,9 @@ def main():
     modes = [a[1] if len(a) > 1 else "" for a in args if a[0].endswith(".so") or a[0] == "torch"]
     rest = [a[0] for a in args if not (a[0].endswith(".so") or a[0] == "torch")]
     rounds = int(rest[0]) if rest else 10
+    if not what.startswith("gemm"):  # the library arm exists for the plain GEMM shapes only
+        keep = [i for i, p in enumerate(paths) if p != "torch"]
+        paths, modes = [paths[i] for i in keep], [modes[i] for i in keep]
     libs = [load(p) if p != "torch" else None for p in paths]
     dev = torch.device("cuda:0")
     st = torch.cuda.current_stream().cuda_stream
