@@ -11,7 +11,8 @@ import os
 from ctypes import c_float, c_int, c_int64, c_void_p, c_char_p, POINTER
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libqie.so")
+# QIE_LIB_PATH: another build of the same library (same-box A/B of whole-model runs, tools/ab_bench.sh)
+LIB_PATH = os.environ.get("QIE_LIB_PATH") or os.path.join(_HERE, "libqie.so")
 
 P = c_void_p
 I = c_int

@@ -227,11 +227,13 @@ __device__ __forceinline__ u32x2_t epi_pre_c(const EpiCols<I8, NT>& c, int i, in
     const float sx = c.sx[i];
     const f32x4_t sw = c.sw[j];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) v[k] = rbf(__builtin_fmaf((float)a[k], sx * sw[k], b4[k]));
+    for (int k = 0; k < 4; ++k) v[k] = __builtin_fmaf((float)a[k], sx * sw[k], b4[k]);
   } else {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) v[k] = rbf(a[k] + b4[k]);
+    for (int k = 0; k < 4; ++k) v[k] = a[k] + b4[k];
   }
+  rbf2(v[0], v[1]);  // the module output's bf16 rounding, two values per conversion
+  rbf2(v[2], v[3]);
   if constexpr (EPI == EPI_GELU) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) v[k] = gelu_tanh_f(v[k]);

@@ -32,8 +32,18 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
 // round an fp32 value to the nearest bf16 and return it as fp32
 __device__ __forceinline__ float rbf(float f) { return bf2f(f2bf(f)); }
 
+// two floats -> two RNE bf16 in one word: ONE v_cvt_pk_bf16_f32 with both operands (the scalar
+// casts cost two conversions, a shift and an or)
+typedef __attribute__((ext_vector_type(2))) float qie_f2_t;
+typedef __attribute__((ext_vector_type(2))) __bf16 qie_b2_t;
 __device__ __forceinline__ unsigned pack2(float lo, float hi) {
-  return (unsigned)f2bf(lo) | ((unsigned)f2bf(hi) << 16);
+  return __builtin_bit_cast(unsigned, __builtin_convertvector((qie_f2_t){lo, hi}, qie_b2_t));
+}
+// round two floats to bf16 and back (the pair form of rbf)
+__device__ __forceinline__ void rbf2(float& a, float& b) {
+  const unsigned p = pack2(a, b);
+  a = __uint_as_float(p << 16);
+  b = __uint_as_float(p & 0xffff0000u);
 }
 __device__ __forceinline__ float lo_f(unsigned u) { return __uint_as_float(u << 16); }
 __device__ __forceinline__ float hi_f(unsigned u) { return __uint_as_float(u & 0xffff0000u); }
@@ -61,9 +71,10 @@ __device__ __forceinline__ float gelu_tanh_f(float x) {
   // torch gelu(approximate="tanh"): 0.5*x*(1+tanh(u)), u = sqrt(2/pi)*(x+0.044715*x^3).
   // Identity 0.5*(1+tanh(u)) = 1/(1+exp(-2u)): one v_exp_f32 + one v_rcp_f32
   // (relative error ~1e-7, far below the bf16 rounding of the result).
-  const float kBeta2Log2e = 2.0f * 0.7978845608028654f * 1.4426950408889634f;
-  const float kKappa = 0.044715f;
-  const float t = kBeta2Log2e * __builtin_fmaf(kKappa * x, x * x, x);
+  // t = 2u log2(e) = x (c1 + c2 x^2): three VALU (mul, fma, mul) before the exp
+  const float c1 = 2.0f * 0.7978845608028654f * 1.4426950408889634f;
+  const float c2 = c1 * 0.044715f;
+  const float t = x * __builtin_fmaf(c2, x * x, c1);
   return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-t));
 }
 
