@@ -811,7 +811,16 @@ __device__ __forceinline__ void ring_epilogue(typename MfmaOp<I8>::acc (&acc)[8]
         const auto sx = __builtin_amdgcn_permlane16_swap(a.x, b.x, false, false);
         const auto sy = __builtin_amdgcn_permlane16_swap(a.y, b.y, false, false);
         const int n = nb + (g & 1) * 16 + (g >> 1) * 8;
+#ifdef QIE_EPI_ABL  // timing ablation (wrong results): 1 compute but do not store, 2 store without computing
+        if constexpr (QIE_EPI_ABL == 1) {
+          u32x4_t v = u32x4_t{sx[0], sy[0], sx[1], sy[1]};
+          asm volatile("" ::"v"(v));
+        } else if (m < M && n < N) {
+          epi_store8<EPI>(e, m, n, u32x4_t{(uint32_t)m, (uint32_t)n, 0u, 0u});
+        }
+#else
         if (m < M && n < N) epi_store8<EPI>(e, m, n, u32x4_t{sx[0], sy[0], sx[1], sy[1]});
+#endif
       }
     }
   }
