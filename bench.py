@@ -140,6 +140,8 @@ def main():
                          "latency-oriented split rule ops.splitk_splits)")
     ap.add_argument("--no-text-overlap", action="store_true",
                     help="A/B: run the text stream on the caller's stream, not on a second HIP stream")
+    ap.add_argument("--no-mod-cache", action="store_true",
+                    help="recompute the timestep MLP + modulation vectors every forward (A/B switch)")
     ap.add_argument("--no-batched-mod", action="store_true",
                     help="A/B: one modulation GEMV launch per block and stream, not one for all blocks")
     ap.add_argument("--force-dist", action="store_true",
@@ -171,6 +173,7 @@ def main():
     model.fuse_qk_norm_rope = not args.no_qk_fusion
     model.log2q_attention = not args.no_log2q
     model.batched_modulation = not args.no_batched_mod
+    model.cache_modulation = not args.no_mod_cache
     model.text_splits = args.text_splits or None
     decode = args.vae in ("both", "decode")
     encode = args.vae == "both"

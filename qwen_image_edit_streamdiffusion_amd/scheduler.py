@@ -118,4 +118,10 @@ class FlowMatchEulerDiscreteScheduler:
 def model_timesteps(timesteps_1000: Sequence[float], device) -> torch.Tensor:
     """Pipeline convention [U]: ``t.expand(B).to(bf16)`` then ``/ 1000`` in bf16."""
     t = torch.tensor([float(x) for x in timesteps_1000], dtype=torch.float32)
-    return (t.to(torch.bfloat16) / 1000).to(torch.bfloat16).to(device)
+    tb = (t.to(torch.bfloat16) / 1000).to(torch.bfloat16)
+    r = tb.to(device)
+    # host copy of the values (bf16 bits): the transformer keys its modulation cache on it without
+    # reading the device tensor back; _version guards against later in-place changes
+    r._qie_host = tuple(int(v) for v in tb.view(torch.int16).tolist())
+    r._qie_version = r._version
+    return r

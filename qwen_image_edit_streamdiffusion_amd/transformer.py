@@ -21,6 +21,7 @@ HBM layout per forward (B rows, S_img image tokens, S_txt text tokens):
 from __future__ import annotations
 
 import contextlib
+from collections import OrderedDict
 from dataclasses import dataclass
 from typing import Dict, Iterator, List, Optional, Sequence, Tuple
 
@@ -211,6 +212,13 @@ class QwenImageTransformer2DModel(nn.Module):
         # all 120 modulation GEMVs as one launch before the blocks; False: one launch per block and
         # stream, inside the block (A/B switch)
         self.batched_modulation = True
+        # Modulation cache ("precompute once per (timestep, LoRA) and cache"):
+        # the timestep MLP, the 120 AdaLN modulation vectors and norm_out's vector depend only on
+        # the weights and the per-row timesteps, which repeat every forward in the stream-batch
+        # loop. Keyed on the host copy of the timestep values (scheduler.model_timesteps tags its
+        # tensors); cleared whenever weights change. False: recompute every forward (A/B switch).
+        self.cache_modulation = True
+        self._mod_cache: "OrderedDict[tuple, tuple]" = OrderedDict()
         # K % 64 requirement of the GEMM kernels for the small input projections
         if in_channels % 64 or joint_attention_dim % 64:
             raise NotImplementedError("in_channels and joint_attention_dim must be multiples of 64")
@@ -344,7 +352,12 @@ class QwenImageTransformer2DModel(nn.Module):
         self._ws.clear()
         return self
 
+    def clear_modulation_cache(self):
+        """Drop cached modulation vectors (call after changing weights outside the loaders)."""
+        self._mod_cache.clear()
+
     def _requantize_if_needed(self):
+        self._mod_cache.clear()
         if self.int8_only:
             raise RuntimeError("this model was loaded pre-quantised (int8_only): its bf16 linear weights "
                                "are absent, so they cannot be changed and re-quantised; fuse LoRA "
@@ -373,6 +386,7 @@ class QwenImageTransformer2DModel(nn.Module):
     @torch.no_grad()
     def load_int8_state_dict(self, sd: Dict[str, torch.Tensor]):
         """Inverse of :meth:`int8_state_dict` (strict: every key, every shape)."""
+        self._mod_cache.clear()
         bufs = dict(self.named_buffers())
         skip = {f"w_{n}" for n in self._I8_LINEARS}
         want = {n for n in bufs if n.split(".")[-1] not in skip}
@@ -464,17 +478,22 @@ class QwenImageTransformer2DModel(nn.Module):
             t_bf = ws.t_bf
             t_bf.copy_(t.to(BF16).expand(B))
         icos, isin, tcos, tsin = self._rope_tables(shapes, S_txt)
+        t_key = None
+        host = getattr(timestep, "_qie_host", None)
+        if (self.cache_modulation and self.batched_modulation and host is not None and len(host) in (1, B)
+                and timestep._version == getattr(timestep, "_qie_version", None)):
+            t_key = (tuple(host) * (B // len(host)), B)
         if out is None:
             out = torch.empty(B, S_img, cfg.patch_size ** 2 * cfg.out_channels, dtype=BF16,
                               device=self.device)
         self._forward_impl(ws, x_in, enc, t_bf, B, S_img, S_txt, txt_seq_lens, icos, isin, tcos, tsin,
-                           out.view(B * S_img, -1))
+                           out.view(B * S_img, -1), t_key)
         if not return_dict:
             return (out,)
         return Transformer2DModelOutput(sample=out)
 
     def _forward_impl(self, ws: _Workspace, x_in, enc, t_bf, B, S_img, S_txt, txt_lens, icos, isin, tcos,
-                      tsin, out2d):
+                      tsin, out2d, t_key=None):
         cfg = self.config
         D = cfg.inner_dim
         eps = 1e-6
@@ -485,13 +504,25 @@ class QwenImageTransformer2DModel(nn.Module):
         if has_txt:
             ops.rmsnorm(enc, self.txt_norm_w, out=ws.txt_norm[:R_t], eps=eps)
             ops.linear(ws.txt_norm[:R_t], self.txt_in_w, self.txt_in_b, out=ws.x_txt[:R_t])
-        ops.timestep_embed(t_bf, 256, out=ws.tproj)
-        ops.gemv(ws.tproj, self.t_l1_w, self.t_l1_b, out=ws.t_h)
-        ops.silu(ws.t_h, out=ws.t_hs)
-        ops.gemv(ws.t_hs, self.t_l2_w, self.t_l2_b, out=ws.temb)
-        ops.silu(ws.temb, out=ws.stemb)
-        if self.batched_modulation:
-            ops.gemv(ws.stemb, self._mod_w, self._mod_b, out=ws.mod_all)
+        hit = self._mod_cache.get(t_key) if t_key is not None else None
+        if hit is not None:  # same weights, same per-row timesteps: the vectors of a previous forward
+            self._mod_cache.move_to_end(t_key)
+            ws.mod_all.copy_(hit[0])
+            ws.emb_out.copy_(hit[1])
+        else:
+            ops.timestep_embed(t_bf, 256, out=ws.tproj)
+            ops.gemv(ws.tproj, self.t_l1_w, self.t_l1_b, out=ws.t_h)
+            ops.silu(ws.t_h, out=ws.t_hs)
+            ops.gemv(ws.t_hs, self.t_l2_w, self.t_l2_b, out=ws.temb)
+            ops.silu(ws.temb, out=ws.stemb)
+            if self.batched_modulation:
+                ops.gemv(ws.stemb, self._mod_w, self._mod_b, out=ws.mod_all)
+            # head modulation (AdaLayerNormContinuous, scale first): depends on temb only
+            ops.gemv(ws.stemb, self.norm_out_w, self.norm_out_b, out=ws.emb_out)
+            if t_key is not None:
+                self._mod_cache[t_key] = (ws.mod_all.clone(), ws.emb_out.clone())
+                while len(self._mod_cache) > 8:
+                    self._mod_cache.popitem(last=False)
         kv_len = [S_img + l for l in txt_lens]
         side = self._side_stream() if has_txt else None
         if side is not None:  # the text stream starts from the prologue's x_txt and stemb
@@ -500,8 +531,7 @@ class QwenImageTransformer2DModel(nn.Module):
             self._block(blk, ws, B, S_img, S_txt, kv_len, icos, isin, tcos, tsin, eps, side)
         if side is not None:  # the next forward's prologue rewrites x_txt
             torch.cuda.current_stream().wait_stream(side)
-        # ---- head: AdaLayerNormContinuous (scale first) + proj_out
-        ops.gemv(ws.stemb, self.norm_out_w, self.norm_out_b, out=ws.emb_out)
+        # ---- head: AdaLayerNormContinuous (scale first; emb_out from the prologue) + proj_out
         ops.layernorm_modulate(ws.x_img, ws.emb_out[:, D:], ws.emb_out[:, :D], S_img, out=ws.h_img,
                                eps=eps)
         ops.linear(ws.h_img, self.proj_out_w, self.proj_out_b, out=out2d)

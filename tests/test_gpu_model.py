@@ -247,3 +247,43 @@ def test_pipeline_two_condition_images(dev, tiny):
     assert a.shape == (1, 128, 128, 3) and torch.equal(a, b)
     with pytest.raises(ValueError):
         pipe(image_latents=lat, cond_shape=shapes[:1], generator=torch.Generator().manual_seed(42), **kw)
+
+
+def test_modulation_cache_bitwise_and_invalidated(dev, tiny):
+    """The cached modulation vectors (keyed on scheduler.model_timesteps' host values) give the
+    same forward bit for bit, alternate between two keys like the stream engine, and are dropped
+    when the weights change."""
+    from qwen_image_edit_streamdiffusion_amd import weights as W
+    from qwen_image_edit_streamdiffusion_amd.scheduler import model_timesteps
+    cfg, params, _ = tiny
+    m = make_model(cfg, params, dev)
+    shapes = [(1, 8, 8), (1, 8, 8)]
+    hs, enc = _inputs(2, shapes, 16, cfg.joint_attention_dim, seed=3)
+    hs, enc = hs.to(dev), enc.to(dev)
+    ta, tb = model_timesteps([1000.0, 20.0], dev), model_timesteps([20.0, 1000.0], dev)
+
+    def run(t):
+        return m(hs, enc, None, t, [shapes] * 2, [16, 16], return_dict=False)[0].clone()
+
+    m.cache_modulation = False
+    ref_a, ref_b = run(ta), run(tb)
+    m.cache_modulation = True
+    outs = [run(ta), run(tb), run(ta), run(tb)]  # miss, miss, hit, hit
+    assert len(m._mod_cache) == 2
+    for o, r in zip(outs, [ref_a, ref_b, ref_a, ref_b]):
+        assert torch.equal(o, r)
+    # an untagged tensor (no host copy) is never cached
+    m(hs, enc, None, ta.clone(), [shapes] * 2, [16, 16], return_dict=False)
+    assert len(m._mod_cache) == 2
+    # weights change -> cache dropped, new result
+    D = cfg.inner_dim
+    g = torch.Generator().manual_seed(9)
+    sd = {"transformer_blocks.0.img_mod.1.lora_A.weight": torch.randn(4, D, generator=g) * 0.1,
+          "transformer_blocks.0.img_mod.1.lora_B.weight": torch.randn(6 * D, 4, generator=g) * 0.1}
+    W.fuse_lora(m, sd)
+    assert len(m._mod_cache) == 0
+    m.cache_modulation = False
+    ref_new = run(ta)
+    m.cache_modulation = True
+    assert torch.equal(run(ta), ref_new) and torch.equal(run(ta), ref_new)
+    assert not torch.equal(ref_new, ref_a)
