@@ -36,13 +36,16 @@ __device__ __forceinline__ u32x2_t quant8(const float f[8], float inv) {
   return u32x2_t{w[0], w[1]};
 }
 
+#ifndef QIE_LNMOD_YR  // y never aliases x / shift / scale: lets hipcc hoist chunk i+1's scale / shift
+#define QIE_LNMOD_YR __restrict__  // loads above chunk i's store (one round trip per row, not six)
+#endif
 #ifndef QIE_LNMOD_PREFETCH
 #define QIE_LNMOD_PREFETCH 0  // measured slower: 42.0 vs 39.3 us (register pressure), kept as a build option
 #endif
 template <bool I8>
 __global__ void __launch_bounds__(256)
     ln_mod_kernel(const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __restrict__ shift,
-                  const bf16_t* __restrict__ scale, int64_t mod_bstride, int rpb, void* y, int64_t ldy,
+                  const bf16_t* __restrict__ scale, int64_t mod_bstride, int rpb, void* QIE_LNMOD_YR y, int64_t ldy,
                   float* qscale, int rows, int D, float eps) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;

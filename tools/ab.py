@@ -138,6 +138,21 @@ def main():
                 x.data_ptr(), K, w.data_ptr(), b.data_ptr(), outs[i].data_ptr(), M, K, S_IMG, 0, B, H, Dh, S_PAD,
                 nq.data_ptr(), nk.data_ptr(), cos_t.data_ptr(), sin_t.data_ptr(), 1e-6, 1.0, st)
             assert rc == 0, rc
+    elif what == "lnmod":  # LayerNorm + modulate of the image rows (B = 2 stream batch)
+        M, D = 16384, 3072
+        x = torch.randn(M, D, device=dev).to(BF16)
+        mod = (torch.randn(2, 6 * D, device=dev) * 0.1).to(BF16)
+        outs = [torch.empty(M, D, dtype=BF16, device=dev) for _ in libs]
+        flops = 4.0 * M * D  # bytes moved (read + write), reported as "TFLOP/s" = TB/s here
+        for lib in libs:
+            lib.qie_layernorm_modulate_bf16.argtypes = [
+                ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int,
+                ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_void_p]
+
+        def run(i):
+            rc = libs[i].qie_layernorm_modulate_bf16(x.data_ptr(), D, mod.data_ptr(), mod[:, D:].data_ptr(), 6 * D,
+                                                     M // 2, outs[i].data_ptr(), D, M, D, 1e-6, st)
+            assert rc == 0, rc
     elif what.startswith("gemm"):
         if what.startswith("gemm:"):  # gemm:M:N:K
             M, N, K = (int(v) for v in what.split(":")[1:])
