@@ -2315,18 +2315,60 @@ __global__ void __launch_bounds__(WM * 2 * 64)
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
+#ifndef QIE_CONV_EPI_PRELOAD  // 0: epilogue4 per accumulator tile (bias / residual loads between stores)
+#define QIE_CONV_EPI_PRELOAD 1
+#endif
+  if constexpr (!QIE_CONV_EPI_PRELOAD || (EPI != EPI_BIAS && EPI != EPI_RES)) {
 #pragma unroll
-  for (int i = 0; i < MT; ++i) {
-    const int m = m0 + wm * TM + i * 16 + fr;
-    if (m >= M) continue;
+    for (int i = 0; i < MT; ++i) {
+      const int m = m0 + wm * TM + i * 16 + fr;
+      if (m >= M) continue;
 #pragma unroll
-    for (int j = 0; j < NTL; ++j) {
-      const int n = n0 + wn * TN + j * 16 + (lane >> 4) * 4;
-      if (n >= N) continue;
-      float v[4];
+      for (int j = 0; j < NTL; ++j) {
+        const int n = n0 + wn * TN + j * 16 + (lane >> 4) * 4;
+        if (n >= N) continue;
+        float v[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r];
-      epilogue4<EPI, false>(e, m, n, v);
+        for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r];
+        epilogue4<EPI, false>(e, m, n, v);
+      }
+    }
+  } else {
+    // every operand of the wave's stores loaded first -- the bias of its NTL column tiles and, for
+    // the ResidualBlock sum, the residual it overwrites -- in one round trip: loaded between the
+    // stores, each would wait behind the previous store (possible alias), MT * NTL round trips
+    u32x2_t bw[NTL], xw[MT][NTL];
+#pragma unroll
+    for (int j = 0; j < NTL; ++j) bw[j] = *(const u32x2_t*)(e.bias + min(n0 + wn * TN + j * 16 + (lane >> 4) * 4, N - 4));
+    if constexpr (EPI == EPI_RES) {
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NTL; ++j) {
+          const int m = min(m0 + wm * TM + i * 16 + fr, M - 1);
+          const int n = min(n0 + wn * TN + j * 16 + (lane >> 4) * 4, N - 4);
+          xw[i][j] = *(const u32x2_t*)((const bf16_t*)e.out + (int64_t)m * e.ldo + n);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      const int m = m0 + wm * TM + i * 16 + fr;
+#pragma unroll
+      for (int j = 0; j < NTL; ++j) {
+        const int n = n0 + wn * TN + j * 16 + (lane >> 4) * 4;
+        float v[4] = {acc[i][j][0] + lo_f(bw[j].x), acc[i][j][1] + hi_f(bw[j].x), acc[i][j][2] + lo_f(bw[j].y),
+                      acc[i][j][3] + hi_f(bw[j].y)};
+        rbf2(v[0], v[1]);
+        rbf2(v[2], v[3]);
+        if constexpr (EPI == EPI_RES) {
+          v[0] += lo_f(xw[i][j].x);
+          v[1] += hi_f(xw[i][j].x);
+          v[2] += lo_f(xw[i][j].y);
+          v[3] += hi_f(xw[i][j].y);
+        }
+        if (m < M && n < N)
+          *(u32x2_t*)((bf16_t*)e.out + (int64_t)m * e.ldo + n) = u32x2_t{pack2(v[0], v[1]), pack2(v[2], v[3])};
+      }
     }
   }
 }
