@@ -530,3 +530,61 @@ def test_linear_splitk_i8_bitwise_equals_unsplit(dev, kind, splits):
         ops.linear_i8(xq, sx, wq, sw, b, a, act=kind)
         ops.linear_splitk_i8(xq, sx, wq, sw, b, kind, c, ws, splits)
     assert torch.equal(a, c)
+
+
+def _gpu_ref_linear(x, w, b):
+    """fp32 torch reference on the device (bf16 inputs, fp32 accumulate, one bf16 rounding)."""
+    return (x.float() @ w.float().t() + b.float()).to(BF16)
+
+
+@pytest.mark.parametrize("M,N,K,act", [
+    (4400, 9216, 3072, 0),   # 18 x 36 = 648 tiles: every work-group of the persistent GEMM runs 2-3 tiles
+    (6000, 3072, 3136, 1),   # 288 tiles, nk = 49 (odd: the LDS slot parity flips from tile to tile), GELU
+    (6016, 4352, 192, 0),    # nk = 3 (the shortest K the big kernels take), ragged M and N tiles
+])
+def test_linear_persistent_multi_tile(dev, M, N, K, act):
+    """The persistent big-shape GEMM (gemm_w4p: one work-group per CU walking several output tiles,
+    the K-tile pipeline crossing tile boundaries) against an fp32 torch reference on the device."""
+    ops = _ops()
+    g = torch.Generator(device=dev).manual_seed(M + N + K)
+    x = torch.randn(M, K, generator=g, device=dev).to(BF16)
+    w = (torch.randn(N, K, generator=g, device=dev) * 0.02).to(BF16)
+    b = (torch.randn(N, generator=g, device=dev) * 0.1).to(BF16)
+    y = ops.linear(x, w, b, act=act)
+    ref = _gpu_ref_linear(x, w, b)
+    if act:
+        ref = torch.nn.functional.gelu(ref.float(), approximate="tanh").to(BF16)
+    close(y, ref)
+
+
+def test_gated_residual_persistent_multi_tile(dev):
+    ops = _ops()
+    B, rpb, N, K = 2, 3000, 3072, 1088  # 24 x 12 = 288 tiles, nk = 17
+    M = B * rpb
+    g = torch.Generator(device=dev).manual_seed(77)
+    x = torch.randn(M, K, generator=g, device=dev).to(BF16)
+    w = (torch.randn(N, K, generator=g, device=dev) * 0.02).to(BF16)
+    b = (torch.randn(N, generator=g, device=dev) * 0.1).to(BF16)
+    gate = (torch.randn(B, N, generator=g, device=dev) * 0.5).to(BF16)
+    resid = torch.randn(M, N, generator=g, device=dev).to(BF16)
+    h = _gpu_ref_linear(x, w, b).float().view(B, rpb, N)
+    ref = (resid.float().view(B, rpb, N) + (gate.float()[:, None, :] * h).to(BF16).float()).to(BF16).view(M, N)
+    ops.linear_gated_residual(x, w, b, gate, rpb, resid)
+    close(resid, ref)
+
+
+def test_linear_i8_persistent_multi_tile(dev):
+    ops = _ops()
+    M, N, K = 6000, 3072, 3200  # 288 tiles, nk = 25 (int8 K tiles of 128)
+    g = torch.Generator().manual_seed(41)
+    xq = torch.randint(-127, 128, (M, K), generator=g, dtype=torch.int8)
+    wq = torch.randint(-127, 128, (N, K), generator=g, dtype=torch.int8)
+    sx = torch.rand(M, generator=g) * 0.01 + 1e-3
+    sw = torch.rand(N, generator=g) * 0.001 + 1e-4
+    b = (torch.randn(N, generator=g) * 0.1).to(BF16)
+    y = torch.empty(M, N, dtype=BF16, device=dev)
+    ops.linear_i8(xq.to(dev), sx.to(dev), wq.to(dev), sw.to(dev), b.to(dev), y)
+    # exact integer accumulation on the device (fp64 holds these int32 sums exactly)
+    acc = xq.to(dev).double() @ wq.to(dev).double().t()
+    ref = (acc * sx.to(dev).double()[:, None] * sw.to(dev).double()[None, :] + b.to(dev).double()).to(BF16)
+    close(y, ref, rel_l2=4e-3, ulps=2)
