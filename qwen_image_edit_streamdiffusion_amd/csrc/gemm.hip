@@ -2292,13 +2292,16 @@ __global__ void __launch_bounds__(WM * 2 * 64)
     const bool more = kt + NS - 1 < nk;
     if (more) {
       char QIE_LDS* nb = smem + ((kt + NS - 1) % NS) * STAGE;
-      stage_x(nb);
-      stage_w((int64_t)(kt + NS - 1) * kRowBytes, nb + A_BYTES);
+#ifndef QIE_CONV_ABL  // timing ablation bits (tools only): 1 no X gather, 2 no W staging, 4 no MFMA
+#define QIE_CONV_ABL 0
+#endif
+      if (!(QIE_CONV_ABL & 1)) stage_x(nb);
+      if (!(QIE_CONV_ABL & 2)) stage_w((int64_t)(kt + NS - 1) * kRowBytes, nb + A_BYTES);
     }
     const char QIE_LDS* at = smem + cur * STAGE;
     const char QIE_LDS* wt = at + A_BYTES;
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
+    for (int kk = 0; kk < ((QIE_CONV_ABL & 4) ? 0 : 2); ++kk) {
       const int cofs = ((kk * 4 + (lane >> 4)) ^ sw) << 4;
       typename Op::frag wf[NTL], af[MT];
 #pragma unroll
@@ -2369,6 +2372,243 @@ __global__ void __launch_bounds__(WM * 2 * 64)
         if (m < M && n < N)
           *(u32x2_t*)((bf16_t*)e.out + (int64_t)m * e.ldo + n) = u32x2_t{pack2(v[0], v[1]), pack2(v[2], v[3])};
       }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Halo-tiled 3x3 convolution (pad 1; MODE 0 same size, MODE 1 with the nearest-2x upsample folded
+// in) for the VAE's big 3x3 convolutions. conv_kernel above gathers every tap's
+// pixels from L2 again (each input byte fetched 9 times) and runs 2-stage K tiles drained each step
+// (timing ablations: its gather alone is 35 % of the time, its MFMA skeleton tops out at 785 TF/s).
+// Here a workgroup owns TH x 32 output pixels x NT output channels:
+//   * the input halo -- (TH + 2) x 34 pixels (MODE 1: (TH / 2 + 2) x 18 source pixels) x 32
+//     channels -- is staged once per 32-channel chunk by LDS-DMA into one of two halo slots (the
+//     next chunk's halo lands while the current one is consumed) and serves all 9 taps;
+//   * K runs chunk-major: step s = (chunk c, tap t), s = 9c + t, K bytes (t * C + 32c) * 2 of the
+//     [Cout][ky][kx][C] weight rows; the step's NT x 32 weight slice streams through a 6-slot LDS
+//     ring, 4 steps ahead;
+//   * 4 waves (WPX along pixel rows x 4 / WPX along output channels), each 4 output rows x 32
+//     columns (8 pixel blocks of 16) x 96 channels: 48 MFMA 16x16x32 per step against 8 + 6
+//     fragment reads; the step's barrier sits halfway through its MFMAs and the next step's
+//     fragments are read behind it, so one wave per SIMD keeps the matrix core fed;
+//   * LDS rows are 64 B (one pixel / one weight row of 32 channels), the 16-byte column XOR-ed
+//     with 2 * bit 2 of the row index: conflict-free for ds_read_b128 at any pixel shift.
+// The weight layout, zero padding and epilogues are conv_kernel's; the fp32 sums run chunk-major,
+// so the rounding order differs from conv_kernel's (not bitwise equal; see tests/test_gpu_vae.py).
+#ifndef QIE_CONV_HALO  // 0: every convolution on conv_kernel
+#define QIE_CONV_HALO 1
+#endif
+#ifndef QIE_CONV_HALO_MIN  // workgroups from which a convolution takes the halo kernel
+#define QIE_CONV_HALO_MIN 256
+#endif
+constexpr int kConvRing = 6, kConvPD = 4;  // weight-ring slots, prefetch distance (steps)
+
+template <int WPX, int MODE>
+struct HaloGeo {
+  static constexpr int WN = 4 / WPX;
+  static constexpr int TH = 4 * WPX, NT = 96 * WN;                 // output tile TH x 32 x NT
+  static constexpr int HW = MODE == 1 ? 18 : 34;                   // halo columns
+  static constexpr int HR = MODE == 1 ? TH / 2 + 2 : TH + 2;       // halo rows
+  static constexpr int HPIX = HR * HW;
+  static constexpr int NH = ((HPIX + 15) / 16 + 3) / 4;            // halo pieces (1 KiB) per wave
+  static constexpr int HBYTES = NH * 4 * 1024;
+  static constexpr int NW = (NT / 16 + 3) / 4;                     // weight pieces per wave
+  static constexpr int WBYTES = NW * 4 * 1024;
+  static constexpr int LDS = 2 * HBYTES + kConvRing * WBYTES;
+  static constexpr int ROWB = (MODE == 1 ? 2 : 4) * HW * 64;       // halo bytes between waves
+};
+
+// s_waitcnt vmcnt(n) + s_barrier: all but the wave's n newest LDS-DMA pieces landed
+template <int n>
+__device__ __forceinline__ void vm_wait_barrier() {
+  static_assert(n >= 0 && n <= 63, "vmcnt");
+  asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"i"(n) : "memory");
+}
+template <int EPI, int WPX, int MODE>
+__global__ void __launch_bounds__(256, 1)
+    conv_halo_kernel(const bf16_t* __restrict__ X, int H_in, int W_in, int C, int H, int Wd,
+                     const char* __restrict__ Wt, int ldw_b, int N, EpiArgs e) {
+  using G = HaloGeo<WPX, MODE>;
+  constexpr int NH = G::NH, NW = G::NW, PD = kConvPD, R = kConvRing;
+  __shared__ __attribute__((aligned(16))) char smem_raw[G::LDS];
+  char QIE_LDS* smem = (char QIE_LDS*)smem_raw;
+
+  const int tiles_x = (Wd + 31) / 32, tiles_y = (H + G::TH - 1) / G::TH, tiles_n = N / G::NT;
+  const int wgid = xcd_remap(blockIdx.x, tiles_x * tiles_y * tiles_n);
+  const int tn = wgid % tiles_n, txy = wgid / tiles_n;
+  const int x0 = (txy % tiles_x) * 32, y0 = (txy / tiles_x) * G::TH, n0 = tn * G::NT;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int wp = wave / G::WN, wn = wave % G::WN;
+  const int fr = lane & 15, g = lane >> 4;
+  const int NC = C / 32;
+
+  // halo pieces of this wave: pixel p = P * 16 + lane / 4, 16-byte column lane % 4
+  const i32x4_t xr = pp_rsrc((const char*)X, H_in * W_in * C * 2);
+  uint32_t hoff[NH];
+#pragma unroll
+  for (int k = 0; k < NH; ++k) {
+    const int p = (wave * NH + k) * 16 + (lane >> 2);
+    const int lc = (lane & 3) ^ (((p >> 2) & 1) << 1);
+    const int hrow = p / G::HW, hcol = p - hrow * G::HW;
+    const int sy = (MODE == 1 ? (y0 >> 1) : y0) - 1 + hrow, sx = (MODE == 1 ? (x0 >> 1) : x0) - 1 + hcol;
+    const bool ok = p < G::HPIX && sy >= 0 && sx >= 0 && sy < H_in && sx < W_in;
+    hoff[k] = ok ? (uint32_t)(((sy * W_in + sx) * C + lc * 8) * 2) : 0x80000000u;
+  }
+  // weight pieces: tile row n = P * 16 + lane / 4
+  const i32x4_t wr = pp_rsrc(Wt + (int64_t)n0 * ldw_b, G::NT * ldw_b);
+  uint32_t woff[NW];
+#pragma unroll
+  for (int k = 0; k < NW; ++k) {
+    const int n = (wave + 4 * k) * 16 + (lane >> 2);
+    const int lc = (lane & 3) ^ (((n >> 2) & 1) << 1);
+    woff[k] = n < G::NT ? (uint32_t)(n * ldw_b + lc * 16) : 0x80000000u;
+  }
+  char QIE_LDS* const wring = smem + 2 * G::HBYTES;
+  auto dma_halo = [&](int c) __attribute__((always_inline)) {  // c == NC reloads chunk 0 (unread)
+    char QIE_LDS* slot = smem + (c & 1) * G::HBYTES;
+    const int soff = c < NC ? c * 64 : 0;
+#pragma unroll
+    for (int k = 0; k < NH; ++k) w4l_dma<0>(xr, slot + (wave * NH + k) * 1024, hoff[k], soff);
+  };
+  auto dma_w = [&](int s) __attribute__((always_inline)) {  // step s = 9c + t: K bytes (t * C + 32 c) * 2
+    const int c = s / 9, t = s - 9 * c;
+    char QIE_LDS* slot = wring + (s % R) * G::WBYTES;
+#pragma unroll
+    for (int k = 0; k < NW; ++k) w4l_dma<0>(wr, slot + (wave + 4 * k) * 1024, woff[k], (t * C + c * 32) * 2);
+  };
+
+  // per-lane pixel-fragment offsets for halo row k (counted from the wave's first row) and tap
+  // column dx: the lane's halo column q and its swizzled 16-byte column. Bit 2 of the pixel index
+  // row * HW + column (HW = 32 + 2 or 16 + 2) is bit 2 of (2 * row) mod 8 + q, so k mod 4 (with
+  // the wave's row base) and dx select it
+  uint32_t aoff[4][3];
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+#pragma unroll
+    for (int dx = 0; dx < 3; ++dx) {
+      const int q = MODE == 1 ? ((fr + dx - 1) >> 1) + 1 : fr + dx;   // halo column within the block
+      const int hrow2 = (2 * ((MODE == 1 ? 2 : 4) * wp + k)) & 7;     // (2 * absolute halo row) mod 8
+      const int col = g ^ ((((hrow2 + q) >> 2) & 1) << 1);
+      aoff[k][dx] = (uint32_t)(q * 64 + col * 16);
+    }
+  const uint32_t hbase = (uint32_t)(uintptr_t)smem + wp * G::ROWB;
+  const uint32_t wlane = (uint32_t)(fr * 64 + ((g ^ (((fr >> 2) & 1) << 1)) << 4)) + wn * 96 * 64;
+  const uint32_t wbase = (uint32_t)(uintptr_t)wring + wlane;
+
+  using acc_t = f32x4_t;
+  acc_t acc[8][6];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 6; ++j) acc[i][j] = acc_t{0, 0, 0, 0};
+
+  // fragments of step (c, T): pixel block b = 2r + h (output row r of the wave, half h)
+  auto read_frags = [&](auto t_t, int c, int s, bf16x8_t (&af)[8], bf16x8_t (&wf)[6]) __attribute__((always_inline)) {
+    constexpr int T = decltype(t_t)::value, dy = T / 3, dx = T % 3;
+    const uint32_t hb = hbase + (c & 1) * G::HBYTES;
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      const int r = b >> 1, h = b & 1;
+      const int k = MODE == 1 ? ((r + dy - 1) >> 1) + 1 : r + dy;
+      const int imm = (k * G::HW + (MODE == 1 ? 8 : 16) * h) * 64;  // the ds_read offset field
+      const char QIE_LDS* pa = (const char QIE_LDS*)(uintptr_t)(hb + aoff[k & 3][dx]);
+      af[b] = *(const bf16x8_t QIE_LDS*)(pa + imm);
+    }
+    const char QIE_LDS* pw = (const char QIE_LDS*)(uintptr_t)(wbase + (s % R) * G::WBYTES);
+#pragma unroll
+    for (int j = 0; j < 6; ++j) wf[j] = *(const bf16x8_t QIE_LDS*)(pw + j * 16 * 64);
+  };
+
+  // one step: prefetch, MFMAs of blocks 0-3, wait + barrier for step s + 1, its fragment reads,
+  // MFMAs of blocks 4-7
+  auto step = [&](auto t_t, int c, bf16x8_t (&af)[8], bf16x8_t (&wf)[6], bf16x8_t (&an)[8],
+                  bf16x8_t (&wn_)[6]) __attribute__((always_inline)) {
+    constexpr int T = decltype(t_t)::value;
+    const int s = 9 * c + T;
+    // branch-free: past the last step the weight pieces, the halo of chunk NC and the fragment
+    // reads of "step S" still run, into slots no remaining step reads (harmless bytes)
+    dma_w(s + PD);
+    if constexpr (T == 1) dma_halo(c + 1);
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+      for (int j = 0; j < 6; ++j) Mma4<false>::acc(acc[b][j], wf[j], af[b]);
+    // step s + 1's weights landed (PD - 1 later weight steps may stay in flight, plus this
+    // chunk's next halo while it is younger than the awaited weights)
+    if constexpr (T >= 1 && T <= PD) vm_wait_barrier<(PD - 1) * NW + NH>();
+    else vm_wait_barrier<(PD - 1) * NW>();
+    read_frags(std::integral_constant<int, (T + 1) % 9>{}, T == 8 ? c + 1 : c, s + 1, an, wn_);
+#pragma unroll
+    for (int b = 4; b < 8; ++b)
+#pragma unroll
+      for (int j = 0; j < 6; ++j) Mma4<false>::acc(acc[b][j], wf[j], af[b]);
+  };
+
+  // prologue: halo 0, weight steps 0 .. PD - 1, then step 0's fragments
+  dma_halo(0);
+#pragma unroll
+  for (int s = 0; s < PD; ++s) dma_w(s);
+  vm_wait_barrier<(PD - 1) * NW>();
+  bf16x8_t a0[8], w0[6], a1[8], w1[6];
+  read_frags(std::integral_constant<int, 0>{}, 0, 0, a0, w0);
+  // two chunks per trip (9 taps alternate the fragment sets, so the parity flips every chunk)
+  for (int c = 0;; c += 2) {
+    static_for<0, 9>([&](auto t_t) __attribute__((always_inline)) {
+      if constexpr (decltype(t_t)::value % 2 == 0) step(t_t, c, a0, w0, a1, w1);
+      else step(t_t, c, a1, w1, a0, w0);
+    });
+    if (c + 1 >= NC) break;
+    static_for<0, 9>([&](auto t_t) __attribute__((always_inline)) {
+      if constexpr (decltype(t_t)::value % 2 == 0) step(t_t, c + 1, a1, w1, a0, w0);
+      else step(t_t, c + 1, a0, w0, a1, w1);
+    });
+    if (c + 2 >= NC) break;
+  }
+
+  // the asm MFMAs' results are read by VALU below: drain the matrix pipe first (hipcc does not
+  // pad inline-asm MFMAs), then redefine the accumulators so no read is hoisted above the wait
+  asm volatile("s_nop 15\n\ts_nop 7" ::: "memory");
+#pragma unroll
+  for (int b = 0; b < 8; ++b)
+    asm volatile("" : "+a"(acc[b][0]), "+a"(acc[b][1]), "+a"(acc[b][2]), "+a"(acc[b][3]), "+a"(acc[b][4]),
+                 "+a"(acc[b][5]));
+
+  // epilogue: bias (and the ResidualBlock residual, in place) loaded before any store
+  const int nb = n0 + wn * 96 + g * 4;
+  u32x2_t bw[6];
+#pragma unroll
+  for (int j = 0; j < 6; ++j) bw[j] = *(const u32x2_t*)(e.bias + nb + j * 16);
+  int mrow[8];
+#pragma unroll
+  for (int b = 0; b < 8; ++b) {
+    const int y = y0 + 4 * wp + (b >> 1), x = x0 + 16 * (b & 1) + fr;
+    mrow[b] = (y < H && x < Wd) ? y * Wd + x : -1;
+  }
+  u32x2_t xw[8][6];
+  if constexpr (EPI == EPI_RES) {
+#pragma unroll
+    for (int b = 0; b < 8; ++b)
+#pragma unroll
+      for (int j = 0; j < 6; ++j)
+        xw[b][j] = *(const u32x2_t*)((const bf16_t*)e.out + (int64_t)max(mrow[b], 0) * e.ldo + nb + j * 16);
+  }
+#pragma unroll
+  for (int b = 0; b < 8; ++b) {
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      float v[4] = {acc[b][j][0] + lo_f(bw[j].x), acc[b][j][1] + hi_f(bw[j].x), acc[b][j][2] + lo_f(bw[j].y),
+                    acc[b][j][3] + hi_f(bw[j].y)};
+      rbf2(v[0], v[1]);
+      rbf2(v[2], v[3]);
+      if constexpr (EPI == EPI_RES) {
+        v[0] += lo_f(xw[b][j].x);
+        v[1] += hi_f(xw[b][j].x);
+        v[2] += lo_f(xw[b][j].y);
+        v[3] += hi_f(xw[b][j].y);
+      }
+      if (mrow[b] >= 0)
+        *(u32x2_t*)((bf16_t*)e.out + (int64_t)mrow[b] * e.ldo + nb + j * 16) = u32x2_t{pack2(v[0], v[1]), pack2(v[2], v[3])};
     }
   }
 }
@@ -2573,6 +2813,32 @@ extern "C" int qie_conv2d_bf16(const void* x, int H_in, int W_in, int C, int mod
   QIE_CHECK_ARG(!resid || resid == y);  // y = bf16(resid + bf16(acc + bias)), in place
   EpiArgs e = make_epi(y, N, bias);
   const char* wc = (const char*)w;
+#if QIE_CONV_HALO
+  // halo-tiled kernel: 3x3, same size or upsampled, 32-channel chunks, 96 / 192-channel tiles,
+  // enough tiles to fill the chip (smaller grids stay on conv_kernel's 128-pixel tiles)
+  if (ksize == 3 && mode != 2 && C % 32 == 0 && (N == 96 || N % 192 == 0) && (int64_t)N * ldw * 2 < (1ll << 31)) {
+    const int wpx = N == 96 ? 4 : 2, th = 4 * wpx, nt = N == 96 ? 96 : 192;
+    const int64_t nwg = (int64_t)((c.W_out + 31) / 32) * ((c.H_out + th - 1) / th) * (N / nt);
+    if (nwg >= QIE_CONV_HALO_MIN) {
+      const bf16_t* xb = (const bf16_t*)x;
+      auto k = [&](auto epi_t, auto wpx_t, auto mode_t) {
+        constexpr int EP = decltype(epi_t)::value, WX = decltype(wpx_t)::value, MD = decltype(mode_t)::value;
+        conv_halo_kernel<EP, WX, MD><<<(int)nwg, 256, 0, s>>>(xb, H_in, W_in, C, c.H_out, c.W_out, wc, (int)(ldw * 2), N, e);
+      };
+      auto by_mode = [&](auto epi_t, auto wpx_t) {
+        if (mode == 1) k(epi_t, wpx_t, std::integral_constant<int, 1>{});
+        else k(epi_t, wpx_t, std::integral_constant<int, 0>{});
+      };
+      auto by_wpx = [&](auto epi_t) {
+        if (wpx == 4) by_mode(epi_t, std::integral_constant<int, 4>{});
+        else by_mode(epi_t, std::integral_constant<int, 2>{});
+      };
+      if (resid) by_wpx(std::integral_constant<int, EPI_RES>{});
+      else by_wpx(std::integral_constant<int, EPI_BIAS>{});
+      return qie_last_error();
+    }
+  }
+#endif
   // 128-pixel tiles (4 waves, 2 workgroups per CU; 256-pixel / 8-wave tiles from QIE_CONV_BIG_MIN
   // workgroups); 96-wide output tiles when N is a multiple of 96 but not of 128 (96, 192)
   const bool n96 = N % 128 != 0 && N % 96 == 0;

@@ -57,6 +57,11 @@ def _nhwc(x):  # [C, H, W] -> [H*W, C]
     (256, 512, 64, 128, 3, "down"),  # stride 2, many workgroups
     (256, 256, 64, 192, 3, False),  # 96-wide output tiles
     (256, 512, 32, 96, 3, False),   # N = 96, C = 32 < 64: multi-tap K tiles
+    # halo-tiled kernel (>= 256 workgroups): ragged edges, both tile shapes, upsampled halo
+    (250, 500, 96, 192, 3, False),  # 8 x 32 tiles x 192 channels, partial tiles at both edges
+    (260, 600, 64, 96, 3, False),   # 16 x 32 tiles x 96 channels, partial tiles
+    (130, 250, 192, 96, 3, True),   # upsampled halo (18 source columns), N = 96
+    (66, 132, 128, 384, 3, True),   # upsampled halo, two 192-channel tiles
 ])
 def test_conv2d(dev, H, W, C, N, k, up):
     from qwen_image_edit_streamdiffusion_amd.vae import conv_weight
@@ -74,6 +79,22 @@ def test_conv2d(dev, H, W, C, N, k, up):
             xi = F.interpolate(xi, scale_factor=2.0, mode="nearest-exact")
         ref = F.conv2d(xi, w4.float().cpu(), b.float().cpu(), padding=k // 2)[0].to(BF16)
     close(y, _nhwc(ref))
+
+
+def test_conv2d_residual_halo(dev):
+    """The ResidualBlock epilogue (in place onto the shortcut) on the halo-tiled kernel's shapes."""
+    from qwen_image_edit_streamdiffusion_amd.vae import conv_weight
+    ops = _ops()
+    for H, W, C, N in ((512, 256, 96, 96), (128, 512, 192, 192)):
+        x = rnd((C, H, W), dev, 1.0, 8)
+        w4 = rnd((N, C, 3, 3), dev, 1.0 / math.sqrt(9 * C), 9)
+        b = rnd((N,), dev, 0.1, 10)
+        h = rnd((N, H, W), dev, 1.0, 11)
+        conv = F.conv2d(x.float().cpu()[None], w4.float().cpu(), b.float().cpu(), padding=1)[0]
+        ref = (conv.to(BF16).float() + h.float().cpu()).to(BF16)
+        out = _nhwc(h)
+        ops.conv2d(_nhwc(x), H, W, conv_weight(w4), b, out=out, residual=True)
+        close(out, _nhwc(ref), ulps=4)
 
 
 def test_conv2d_residual_and_causal3d(dev):
