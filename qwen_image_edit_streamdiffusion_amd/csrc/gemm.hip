@@ -2402,7 +2402,16 @@ __global__ void __launch_bounds__(WM * 2 * 64)
 #ifndef QIE_CONV_HALO_MIN  // workgroups from which a convolution takes the halo kernel
 #define QIE_CONV_HALO_MIN 256
 #endif
-constexpr int kConvRing = 6, kConvPD = 4;  // weight-ring slots, prefetch distance (steps)
+#ifndef QIE_HALO_PD  // weight prefetch distance (steps); the ring has PD + 2 slots
+#define QIE_HALO_PD 4
+#endif
+#ifndef QIE_HALO_PERSIST  // 1: one workgroup per CU walking its tiles; 0: one workgroup per tile
+#define QIE_HALO_PERSIST 1
+#endif
+#ifndef QIE_HALO_ABL  // timing ablations (tools only): 1 no weight DMA, 2 no halo DMA, 4 no MFMA, 8 no fragment reads
+#define QIE_HALO_ABL 0
+#endif
+constexpr int kConvPD = QIE_HALO_PD, kConvRing = QIE_HALO_PD + 2;
 
 template <int WPX, int MODE>
 struct HaloGeo {
@@ -2434,29 +2443,44 @@ __global__ void __launch_bounds__(256, 1)
   __shared__ __attribute__((aligned(16))) char smem_raw[G::LDS];
   char QIE_LDS* smem = (char QIE_LDS*)smem_raw;
 
+  // persistent: this workgroup's tiles are blockIdx.x + i * gridDim.x (n fastest, then x, then
+  // y); the step stream -- weights PD steps ahead, the next chunk's halo -- runs on across its
+  // tiles, so a tile's first steps load while the previous tile's last steps and stores run
   const int tiles_x = (Wd + 31) / 32, tiles_y = (H + G::TH - 1) / G::TH, tiles_n = N / G::NT;
-  const int wgid = xcd_remap(blockIdx.x, tiles_x * tiles_y * tiles_n);
-  const int tn = wgid % tiles_n, txy = wgid / tiles_n;
-  const int x0 = (txy % tiles_x) * 32, y0 = (txy / tiles_x) * G::TH, n0 = tn * G::NT;
+  const int ntiles = tiles_x * tiles_y * tiles_n;
+  const int my_tiles = (ntiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
+  const int NC = C / 32, GC = my_tiles * NC;  // 32-channel chunks over all this workgroup's tiles
+  auto tile_of = [&](int ti, int& x0, int& y0, int& n0) __attribute__((always_inline)) {
+    const int id = (int)blockIdx.x + min(ti, my_tiles - 1) * (int)gridDim.x;
+    const int tn = id % tiles_n, txy = id / tiles_n;
+    x0 = (txy % tiles_x) * 32;
+    y0 = (txy / tiles_x) * G::TH;
+    n0 = tn * G::NT;
+  };
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int wp = wave / G::WN, wn = wave % G::WN;
   const int fr = lane & 15, g = lane >> 4;
-  const int NC = C / 32;
 
-  // halo pieces of this wave: pixel p = P * 16 + lane / 4, 16-byte column lane % 4
+  // halo pieces of this wave: pixel p = P * 16 + lane / 4, 16-byte column lane % 4; a tile past
+  // the workgroup's last loads zeros (out of the buffer's range)
   const i32x4_t xr = pp_rsrc((const char*)X, H_in * W_in * C * 2);
   uint32_t hoff[NH];
+  auto set_hoff = [&](int ti) __attribute__((always_inline)) {
+    int x0, y0, n0;
+    tile_of(ti, x0, y0, n0);
 #pragma unroll
-  for (int k = 0; k < NH; ++k) {
-    const int p = (wave * NH + k) * 16 + (lane >> 2);
-    const int lc = (lane & 3) ^ (((p >> 2) & 1) << 1);
-    const int hrow = p / G::HW, hcol = p - hrow * G::HW;
-    const int sy = (MODE == 1 ? (y0 >> 1) : y0) - 1 + hrow, sx = (MODE == 1 ? (x0 >> 1) : x0) - 1 + hcol;
-    const bool ok = p < G::HPIX && sy >= 0 && sx >= 0 && sy < H_in && sx < W_in;
-    hoff[k] = ok ? (uint32_t)(((sy * W_in + sx) * C + lc * 8) * 2) : 0x80000000u;
-  }
-  // weight pieces: tile row n = P * 16 + lane / 4
-  const i32x4_t wr = pp_rsrc(Wt + (int64_t)n0 * ldw_b, G::NT * ldw_b);
+    for (int k = 0; k < NH; ++k) {
+      const int p = (wave * NH + k) * 16 + (lane >> 2);
+      const int lc = (lane & 3) ^ (((p >> 2) & 1) << 1);
+      const int hrow = p / G::HW, hcol = p - hrow * G::HW;
+      const int sy = (MODE == 1 ? (y0 >> 1) : y0) - 1 + hrow, sx = (MODE == 1 ? (x0 >> 1) : x0) - 1 + hcol;
+      const bool ok = ti < my_tiles && p < G::HPIX && sy >= 0 && sx >= 0 && sy < H_in && sx < W_in;
+      hoff[k] = ok ? (uint32_t)(((sy * W_in + sx) * C + lc * 8) * 2) : 0x80000000u;
+    }
+  };
+  // weight pieces: tile row n = P * 16 + lane / 4 (the tile's first row and the step's K bytes
+  // go in the scalar offset)
+  const i32x4_t wr = pp_rsrc(Wt, N * ldw_b);
   uint32_t woff[NW];
 #pragma unroll
   for (int k = 0; k < NW; ++k) {
@@ -2465,17 +2489,33 @@ __global__ void __launch_bounds__(256, 1)
     woff[k] = n < G::NT ? (uint32_t)(n * ldw_b + lc * 16) : 0x80000000u;
   }
   char QIE_LDS* const wring = smem + 2 * G::HBYTES;
-  auto dma_halo = [&](int c) __attribute__((always_inline)) {  // c == NC reloads chunk 0 (unread)
-    char QIE_LDS* slot = smem + (c & 1) * G::HBYTES;
-    const int soff = c < NC ? c * 64 : 0;
+  auto dma_halo = [&](int gc, int c) __attribute__((always_inline)) {  // global chunk gc = chunk c of its tile
+    char QIE_LDS* slot = smem + (gc & 1) * G::HBYTES;
 #pragma unroll
-    for (int k = 0; k < NH; ++k) w4l_dma<0>(xr, slot + (wave * NH + k) * 1024, hoff[k], soff);
+    for (int k = 0; k < NH; ++k) w4l_dma<0>(xr, slot + (wave * NH + k) * 1024, hoff[k], __builtin_amdgcn_readfirstlane(c * 64));
   };
-  auto dma_w = [&](int s) __attribute__((always_inline)) {  // step s = 9c + t: K bytes (t * C + 32 c) * 2
-    const int c = s / 9, t = s - 9 * c;
+  // the weight stream: (tap wt, chunk wc) of tile wti, K bytes (wt * C + 32 wc) * 2
+  int wt = 0, wc = 0, wti = 0, wn0;
+  {
+    int x0, y0;
+    tile_of(0, x0, y0, wn0);
+  }
+  auto w_advance = [&]() __attribute__((always_inline)) {
+    if (++wt == 9) {
+      wt = 0;
+      if (++wc == NC) {
+        wc = 0;
+        int x0, y0;
+        tile_of(++wti, x0, y0, wn0);
+      }
+    }
+  };
+  auto dma_w = [&](int s) __attribute__((always_inline)) {  // into the slot of global step s
     char QIE_LDS* slot = wring + (s % R) * G::WBYTES;
+    const int soff = __builtin_amdgcn_readfirstlane(wn0 * ldw_b + (wt * C + wc * 32) * 2);
 #pragma unroll
-    for (int k = 0; k < NW; ++k) w4l_dma<0>(wr, slot + (wave + 4 * k) * 1024, woff[k], (t * C + c * 32) * 2);
+    for (int k = 0; k < NW; ++k) w4l_dma<0>(wr, slot + (wave + 4 * k) * 1024, woff[k], soff);
+    w_advance();
   };
 
   // per-lane pixel-fragment offsets for halo row k (counted from the wave's first row) and tap
@@ -2503,114 +2543,172 @@ __global__ void __launch_bounds__(256, 1)
 #pragma unroll
     for (int j = 0; j < 6; ++j) acc[i][j] = acc_t{0, 0, 0, 0};
 
-  // fragments of step (c, T): pixel block b = 2r + h (output row r of the wave, half h)
-  auto read_frags = [&](auto t_t, int c, int s, bf16x8_t (&af)[8], bf16x8_t (&wf)[6]) __attribute__((always_inline)) {
-    constexpr int T = decltype(t_t)::value, dy = T / 3, dx = T % 3;
-    const uint32_t hb = hbase + (c & 1) * G::HBYTES;
-#pragma unroll
-    for (int b = 0; b < 8; ++b) {
-      const int r = b >> 1, h = b & 1;
-      const int k = MODE == 1 ? ((r + dy - 1) >> 1) + 1 : r + dy;
-      const int imm = (k * G::HW + (MODE == 1 ? 8 : 16) * h) * 64;  // the ds_read offset field
-      const char QIE_LDS* pa = (const char QIE_LDS*)(uintptr_t)(hb + aoff[k & 3][dx]);
-      af[b] = *(const bf16x8_t QIE_LDS*)(pa + imm);
+  // fragments of global step s (tap T of global chunk gc): pixel block b = 2r + h (output row r
+  // of the wave, half h). Fragment i of the step (i < 6: weights j = i; then pixel blocks
+  // b = i - 6) is one asm ds_read_b128 with its row offset in the offset field; the reads are
+  // awaited by the lgkmcnt(0) that opens the step which uses them.
+  auto read_frag = [&](auto t_t, auto i_t, int gc, int s, bf16x8_t (&af)[8], bf16x8_t (&wf)[6]) __attribute__((always_inline)) {
+    constexpr int T = decltype(t_t)::value, dy = T / 3, dx = T % 3, i = decltype(i_t)::value;
+    if constexpr (i < 6) {
+      const uint32_t pw = wbase + (s % R) * G::WBYTES;
+      asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(wf[i]) : "v"(pw), "i"(i * 16 * 64));
+    } else {
+      constexpr int b = i - 6, r = b >> 1, h = b & 1;
+      constexpr int k = MODE == 1 ? ((r + dy - 1) >> 1) + 1 : r + dy;
+      constexpr int imm = (k * G::HW + (MODE == 1 ? 8 : 16) * h) * 64;
+      const uint32_t pa = hbase + (gc & 1) * G::HBYTES + aoff[k & 3][dx];
+      asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(af[b]) : "v"(pa), "i"(imm));
     }
-    const char QIE_LDS* pw = (const char QIE_LDS*)(uintptr_t)(wbase + (s % R) * G::WBYTES);
-#pragma unroll
-    for (int j = 0; j < 6; ++j) wf[j] = *(const bf16x8_t QIE_LDS*)(pw + j * 16 * 64);
+  };
+  auto read_frags = [&](auto t_t, int gc, int s, bf16x8_t (&af)[8], bf16x8_t (&wf)[6]) __attribute__((always_inline)) {
+    static_for<0, 14>([&](auto i_t) __attribute__((always_inline)) { read_frag(t_t, i_t, gc, s, af, wf); });
+  };
+  // the step's fragments have landed; every fragment register is redefined behind the wait, so no
+  // copy of one can be scheduled above it
+  auto frags_landed = [&](bf16x8_t (&af)[8], bf16x8_t (&wf)[6]) __attribute__((always_inline)) {
+    asm volatile("s_waitcnt lgkmcnt(0)"
+                 : "+v"(af[0]), "+v"(af[1]), "+v"(af[2]), "+v"(af[3]), "+v"(af[4]), "+v"(af[5]), "+v"(af[6]),
+                   "+v"(af[7]), "+v"(wf[0]), "+v"(wf[1]), "+v"(wf[2]), "+v"(wf[3]), "+v"(wf[4]), "+v"(wf[5])
+                 :
+                 : "memory");
   };
 
-  // one step: prefetch, MFMAs of blocks 0-3, wait + barrier for step s + 1, its fragment reads,
-  // MFMAs of blocks 4-7
-  auto step = [&](auto t_t, int c, bf16x8_t (&af)[8], bf16x8_t (&wf)[6], bf16x8_t (&an)[8],
+  // one step: fragments landed; MFMAs of blocks 0-3 with the step's LDS-DMA pieces (the weights
+  // of step s + PD, at tap 1 the next chunk's halo) one after every second MFMA; wait + barrier
+  // for step s + 1; MFMAs of blocks 4-7 with step s + 1's 14 fragment reads one after each of
+  // the first 14. Branch-free: past the workgroup's last step the weight pieces, a zero halo and
+  // the fragment reads of "step S" still run, into slots no remaining step reads.
+  auto step = [&](auto t_t, int gc, int c, int ti, bf16x8_t (&af)[8], bf16x8_t (&wf)[6], bf16x8_t (&an)[8],
                   bf16x8_t (&wn_)[6]) __attribute__((always_inline)) {
     constexpr int T = decltype(t_t)::value;
-    const int s = 9 * c + T;
-    // branch-free: past the last step the weight pieces, the halo of chunk NC and the fragment
-    // reads of "step S" still run, into slots no remaining step reads (harmless bytes)
-    dma_w(s + PD);
-    if constexpr (T == 1) dma_halo(c + 1);
-#pragma unroll
-    for (int b = 0; b < 4; ++b)
-#pragma unroll
-      for (int j = 0; j < 6; ++j) Mma4<false>::acc(acc[b][j], wf[j], af[b]);
-    // step s + 1's weights landed (PD - 1 later weight steps may stay in flight, plus this
-    // chunk's next halo while it is younger than the awaited weights)
-    if constexpr (T >= 1 && T <= PD) vm_wait_barrier<(PD - 1) * NW + NH>();
+    constexpr bool HALO = T == 1 && !(QIE_HALO_ABL & 2);
+    constexpr int NP = ((QIE_HALO_ABL & 1) ? 0 : NW) + (HALO ? NH : 0);
+    const int s = 9 * gc + T;
+    frags_landed(af, wf);
+    if constexpr (HALO) {  // the next chunk's halo (the next tile's first)
+      if (c + 1 == NC) set_hoff(ti + 1);
+    }
+    char QIE_LDS* const wslot = wring + ((s + PD) % R) * G::WBYTES;
+    const int wsoff = __builtin_amdgcn_readfirstlane(wn0 * ldw_b + (wt * C + wc * 32) * 2);
+    const int gn = gc + 1, cn = c + 1 == NC ? 0 : c + 1;
+    char QIE_LDS* const hslot = smem + (gn & 1) * G::HBYTES;
+    const int hsoff = __builtin_amdgcn_readfirstlane(cn * 64);
+    static_for<0, 24>([&](auto i_t) __attribute__((always_inline)) {
+      constexpr int i = decltype(i_t)::value;
+      if (!(QIE_HALO_ABL & 4)) Mma4<false>::acc(acc[i / 6][i % 6], wf[i % 6], af[i / 6]);
+      if constexpr (i % 2 == 1 && i / 2 < NP) {
+        constexpr int k = i / 2;
+        if constexpr (!(QIE_HALO_ABL & 1) && k < NW) w4l_dma<0>(wr, wslot + (wave + 4 * k) * 1024, woff[k], wsoff);
+        else {
+          constexpr int kh = (QIE_HALO_ABL & 1) ? k : k - NW;
+          w4l_dma<0>(xr, hslot + (wave * NH + kh) * 1024, hoff[kh], hsoff);
+        }
+      }
+    });
+    if (!(QIE_HALO_ABL & 1)) w_advance();
+    // step s + 1's weights landed (PD - 1 later weight steps may stay in flight, plus the next
+    // halo while it is younger than the awaited weights)
+    if constexpr (QIE_HALO_ABL & 3) vm_wait_barrier<0>();
+    else if constexpr (T >= 1 && T <= PD) vm_wait_barrier<(PD - 1) * NW + NH>();
     else vm_wait_barrier<(PD - 1) * NW>();
-    read_frags(std::integral_constant<int, (T + 1) % 9>{}, T == 8 ? c + 1 : c, s + 1, an, wn_);
+    static_for<0, 24>([&](auto i_t) __attribute__((always_inline)) {
+      constexpr int i = decltype(i_t)::value;
+      if (!(QIE_HALO_ABL & 4)) Mma4<false>::acc(acc[4 + i / 6][i % 6], wf[i % 6], af[4 + i / 6]);
+      if constexpr (i < 14 && !(QIE_HALO_ABL & 8))
+        read_frag(std::integral_constant<int, (T + 1) % 9>{}, i_t, T == 8 ? gc + 1 : gc, s + 1, an, wn_);
+    });
+    if constexpr (QIE_HALO_ABL & 8) {
 #pragma unroll
-    for (int b = 4; b < 8; ++b)
+      for (int b = 0; b < 8; ++b) an[b] = af[b];
 #pragma unroll
-      for (int j = 0; j < 6; ++j) Mma4<false>::acc(acc[b][j], wf[j], af[b]);
+      for (int j = 0; j < 6; ++j) wn_[j] = wf[j];
+    }
   };
 
-  // prologue: halo 0, weight steps 0 .. PD - 1, then step 0's fragments
-  dma_halo(0);
+  // a finished tile: bias (and the ResidualBlock residual, in place) loaded before any store,
+  // then the accumulators restart at zero
+  auto epilogue = [&](int x0, int y0, int n0) __attribute__((always_inline)) {
+    // the asm MFMAs' results are read by VALU: drain the matrix pipe first (hipcc does not pad
+    // inline-asm MFMAs), then redefine the accumulators so no read is hoisted above the wait
+    asm volatile("s_nop 15\n\ts_nop 7" ::: "memory");
+#pragma unroll
+    for (int b = 0; b < 8; ++b)
+      asm volatile("" : "+a"(acc[b][0]), "+a"(acc[b][1]), "+a"(acc[b][2]), "+a"(acc[b][3]), "+a"(acc[b][4]),
+                   "+a"(acc[b][5]));
+    const int nb = n0 + wn * 96 + g * 4;
+    u32x2_t bw[6];
+#pragma unroll
+    for (int j = 0; j < 6; ++j) bw[j] = *(const u32x2_t*)(e.bias + nb + j * 16);
+    int mrow[8];
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      const int y = y0 + 4 * wp + (b >> 1), x = x0 + 16 * (b & 1) + fr;
+      mrow[b] = (y < H && x < Wd) ? y * Wd + x : -1;
+    }
+    u32x2_t xw[8][6];
+    if constexpr (EPI == EPI_RES) {
+#pragma unroll
+      for (int b = 0; b < 8; ++b)
+#pragma unroll
+        for (int j = 0; j < 6; ++j)
+          xw[b][j] = *(const u32x2_t*)((const bf16_t*)e.out + (int64_t)max(mrow[b], 0) * e.ldo + nb + j * 16);
+    }
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+#pragma unroll
+      for (int j = 0; j < 6; ++j) {
+        float v[4] = {acc[b][j][0] + lo_f(bw[j].x), acc[b][j][1] + hi_f(bw[j].x), acc[b][j][2] + lo_f(bw[j].y),
+                      acc[b][j][3] + hi_f(bw[j].y)};
+        rbf2(v[0], v[1]);
+        rbf2(v[2], v[3]);
+        if constexpr (EPI == EPI_RES) {
+          v[0] += lo_f(xw[b][j].x);
+          v[1] += hi_f(xw[b][j].x);
+          v[2] += lo_f(xw[b][j].y);
+          v[3] += hi_f(xw[b][j].y);
+        }
+        if (mrow[b] >= 0)
+          *(u32x2_t*)((bf16_t*)e.out + (int64_t)mrow[b] * e.ldo + nb + j * 16) = u32x2_t{pack2(v[0], v[1]), pack2(v[2], v[3])};
+        acc[b][j] = acc_t{0, 0, 0, 0};
+      }
+    }
+  };
+
+  // prologue: tile 0's first halo chunk, weight steps 0 .. PD - 1, then step 0's fragments
+  set_hoff(0);
+  dma_halo(0, 0);
 #pragma unroll
   for (int s = 0; s < PD; ++s) dma_w(s);
   vm_wait_barrier<(PD - 1) * NW>();
   bf16x8_t a0[8], w0[6], a1[8], w1[6];
   read_frags(std::integral_constant<int, 0>{}, 0, 0, a0, w0);
-  // two chunks per trip (9 taps alternate the fragment sets, so the parity flips every chunk)
-  for (int c = 0;; c += 2) {
-    static_for<0, 9>([&](auto t_t) __attribute__((always_inline)) {
-      if constexpr (decltype(t_t)::value % 2 == 0) step(t_t, c, a0, w0, a1, w1);
-      else step(t_t, c, a1, w1, a0, w0);
-    });
-    if (c + 1 >= NC) break;
-    static_for<0, 9>([&](auto t_t) __attribute__((always_inline)) {
-      if constexpr (decltype(t_t)::value % 2 == 0) step(t_t, c + 1, a1, w1, a0, w0);
-      else step(t_t, c + 1, a0, w0, a1, w1);
-    });
-    if (c + 2 >= NC) break;
-  }
-
-  // the asm MFMAs' results are read by VALU below: drain the matrix pipe first (hipcc does not
-  // pad inline-asm MFMAs), then redefine the accumulators so no read is hoisted above the wait
-  asm volatile("s_nop 15\n\ts_nop 7" ::: "memory");
-#pragma unroll
-  for (int b = 0; b < 8; ++b)
-    asm volatile("" : "+a"(acc[b][0]), "+a"(acc[b][1]), "+a"(acc[b][2]), "+a"(acc[b][3]), "+a"(acc[b][4]),
-                 "+a"(acc[b][5]));
-
-  // epilogue: bias (and the ResidualBlock residual, in place) loaded before any store
-  const int nb = n0 + wn * 96 + g * 4;
-  u32x2_t bw[6];
-#pragma unroll
-  for (int j = 0; j < 6; ++j) bw[j] = *(const u32x2_t*)(e.bias + nb + j * 16);
-  int mrow[8];
-#pragma unroll
-  for (int b = 0; b < 8; ++b) {
-    const int y = y0 + 4 * wp + (b >> 1), x = x0 + 16 * (b & 1) + fr;
-    mrow[b] = (y < H && x < Wd) ? y * Wd + x : -1;
-  }
-  u32x2_t xw[8][6];
-  if constexpr (EPI == EPI_RES) {
-#pragma unroll
-    for (int b = 0; b < 8; ++b)
-#pragma unroll
-      for (int j = 0; j < 6; ++j)
-        xw[b][j] = *(const u32x2_t*)((const bf16_t*)e.out + (int64_t)max(mrow[b], 0) * e.ldo + nb + j * 16);
-  }
-#pragma unroll
-  for (int b = 0; b < 8; ++b) {
-#pragma unroll
-    for (int j = 0; j < 6; ++j) {
-      float v[4] = {acc[b][j][0] + lo_f(bw[j].x), acc[b][j][1] + hi_f(bw[j].x), acc[b][j][2] + lo_f(bw[j].y),
-                    acc[b][j][3] + hi_f(bw[j].y)};
-      rbf2(v[0], v[1]);
-      rbf2(v[2], v[3]);
-      if constexpr (EPI == EPI_RES) {
-        v[0] += lo_f(xw[b][j].x);
-        v[1] += hi_f(xw[b][j].x);
-        v[2] += lo_f(xw[b][j].y);
-        v[3] += hi_f(xw[b][j].y);
-      }
-      if (mrow[b] >= 0)
-        *(u32x2_t*)((bf16_t*)e.out + (int64_t)mrow[b] * e.ldo + nb + j * 16) = u32x2_t{pack2(v[0], v[1]), pack2(v[2], v[3])};
+  int cx0, cy0, cn0, ti = 0, c = 0;
+  tile_of(0, cx0, cy0, cn0);
+  auto chunk_end = [&]() __attribute__((always_inline)) {
+    if (c + 1 == NC) {
+      epilogue(cx0, cy0, cn0);
+      tile_of(++ti, cx0, cy0, cn0);
+      c = 0;
+    } else {
+      ++c;
     }
+  };
+  // two chunks per trip (9 taps alternate the fragment sets, so the parity flips every chunk)
+  for (int gc = 0;; gc += 2) {
+    static_for<0, 9>([&](auto t_t) __attribute__((always_inline)) {
+      if constexpr (decltype(t_t)::value % 2 == 0) step(t_t, gc, c, ti, a0, w0, a1, w1);
+      else step(t_t, gc, c, ti, a1, w1, a0, w0);
+    });
+    chunk_end();
+    if (gc + 1 >= GC) break;
+    static_for<0, 9>([&](auto t_t) __attribute__((always_inline)) {
+      if constexpr (decltype(t_t)::value % 2 == 0) step(t_t, gc + 1, c, ti, a1, w1, a0, w0);
+      else step(t_t, gc + 1, c, ti, a0, w0, a1, w1);
+    });
+    chunk_end();
+    if (gc + 2 >= GC) break;
   }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // the trailing pieces land before exit
 }
 
 EpiArgs make_epi(void* out, int64_t ldo, const void* bias) {
@@ -2821,9 +2919,17 @@ extern "C" int qie_conv2d_bf16(const void* x, int H_in, int W_in, int C, int mod
     const int64_t nwg = (int64_t)((c.W_out + 31) / 32) * ((c.H_out + th - 1) / th) * (N / nt);
     if (nwg >= QIE_CONV_HALO_MIN) {
       const bf16_t* xb = (const bf16_t*)x;
+      if (g_cu_count == 0) {
+        int dev = 0, cu = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cu <= 0)
+          cu = 256;
+        g_cu_count = cu;
+      }
+      const int grid = QIE_HALO_PERSIST ? (int)std::min<int64_t>(nwg, g_cu_count) : (int)nwg;
       auto k = [&](auto epi_t, auto wpx_t, auto mode_t) {
         constexpr int EP = decltype(epi_t)::value, WX = decltype(wpx_t)::value, MD = decltype(mode_t)::value;
-        conv_halo_kernel<EP, WX, MD><<<(int)nwg, 256, 0, s>>>(xb, H_in, W_in, C, c.H_out, c.W_out, wc, (int)(ldw * 2), N, e);
+        conv_halo_kernel<EP, WX, MD><<<grid, 256, 0, s>>>(xb, H_in, W_in, C, c.H_out, c.W_out, wc, (int)(ldw * 2), N, e);
       };
       auto by_mode = [&](auto epi_t, auto wpx_t) {
         if (mode == 1) k(epi_t, wpx_t, std::integral_constant<int, 1>{});
