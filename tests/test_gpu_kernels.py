@@ -198,6 +198,23 @@ def test_qkv_norm_rope_fused(dev, B, rpb, H, K, off, s_pad, hw, q_scale):
         close(fused[which, :, :, sl], ref, rel_l2=8e-3, ulps=4)
 
 
+def test_qkv_norm_rope_fused_headline_persistent(dev):
+    """The headline image QKV (B = 2 x 8192 rows, 24 heads, K = 3072): 2304 tiles, so each
+    persistent work-group runs ~9 tiles with the norm + RoPE epilogue between them; == the
+    two-launch path within the GEMM tolerance, V bitwise."""
+    ops = _ops()
+    B, rpb, H, K, s_pad = 2, 8192, 24, 3072, 8448
+    x, w, b, nq, nk, ic, is_, _ = _qkv_nr_case(dev, B, rpb, H, K, 0, s_pad, 74, (64, 64))
+    fused = torch.zeros(3, B, H, s_pad, 128, dtype=BF16, device=dev)
+    ops.linear_qkv_norm_rope(x, w, b, fused, rpb, 0, nq, nk, ic, is_, q_scale=0.12752)
+    two = torch.zeros_like(fused)
+    ops.linear_qkv(x, w, b, two, rpb, 0)
+    ops.qk_norm_rope(two, 0, rpb, nq, nk, ic, is_, q_scale=0.12752)
+    close(fused[:, :, :, :rpb], two[:, :, :, :rpb])
+    assert torch.equal(fused[2], two[2])
+    assert (fused[:, :, :, rpb:] == 0).all()
+
+
 def test_qkv_norm_rope_fused_i8(dev):
     ops = _ops()
     B, rpb, H, K = 2, 2048, 8, 256
