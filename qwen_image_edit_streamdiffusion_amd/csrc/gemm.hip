@@ -504,7 +504,9 @@ struct Mma4<true> {
 #ifndef QIE_GATE_UNIFORM  // gated-residual epilogue: one gate load + 8-row residual round trip
 #define QIE_GATE_UNIFORM 1
 #endif
-template <int NT, int EPI, bool I8>
+// LDS_OK: the workgroup's LDS is free here (false in gemm_w4p, whose slots hold the next tile): the
+// QKV + norm + RoPE form then loads its RoPE rows from the fp32 tables into registers instead.
+template <int NT, int EPI, bool I8, bool LDS_OK = true>
 __device__ __forceinline__ void ring_epilogue(typename MfmaOp<I8>::acc (&acc)[8][NT], const EpiArgs& e, int M,
                                               int N, int mrow0, int ncol0, int lane, char QIE_LDS* smem) {
   // MFMA D -> VALU read hazard (the MFMAs are inline asm, so hipcc pads nothing): 23 wait states
@@ -565,6 +567,18 @@ __device__ __forceinline__ void ring_epilogue(typename MfmaOp<I8>::acc (&acc)[8]
       bool done = false;
       if constexpr (EPI == EPI_QKV_NR) {
         if (which < 2) {
+          // register path (NT == 8, no LDS): the RoPE row of row group i (its 4 column pairs) is
+          // loaded one group ahead of its use, group 0 before pass 1, under its arithmetic
+          auto rope_row = [&](int i, f32x4_t (&cs)[4], f32x4_t (&sn)[4]) {
+            const int64_t o = (int64_t)(min(mrow0 + i * 16 + fr, M - 1) % e.rows_per_batch) * 64 + (dl >> 1);
+#pragma unroll
+            for (int jp = 0; jp < 4; ++jp) {
+              cs[jp] = *(const f32x4_t*)(e.rcos + o + jp * 16);
+              sn[jp] = *(const f32x4_t*)(e.rsin + o + jp * 16);
+            }
+          };
+          f32x4_t rcs[2][4], rsn[2][4];
+          if constexpr (NT == 8 && !LDS_OK) rope_row(0, rcs[0], rsn[0]);
           // pass 1: sum of squares of the rounded values over each 64-column half of the head
           // (the same order in both forms), the two halves added last
           auto half_ss = [&](int i, int hh) {
@@ -602,6 +616,32 @@ __device__ __forceinline__ void ring_epilogue(typename MfmaOp<I8>::acc (&acc)[8]
           }
           const bf16_t* nw = which == 0 ? e.nq : e.nk;
           const float osc = which == 0 ? e.qscale : 1.0f;
+          if constexpr (NT == 8 && !LDS_OK) {
+            u32x4_t wwv[4];
+#pragma unroll
+            for (int jp = 0; jp < 4; ++jp) wwv[jp] = *(const u32x4_t*)(nw + jp * 32 + dl);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+              if (i < 7) rope_row(i + 1, rcs[(i + 1) & 1], rsn[(i + 1) & 1]);
+              const int m = mrow0 + i * 16 + fr;
+#pragma unroll
+              for (int jp = 0; jp < 4; ++jp) {
+                const uint32_t wv[4] = {wwv[jp].x, wwv[jp].y, wwv[jp].z, wwv[jp].w};
+                const f32x4_t cs = rcs[i & 1][jp], sn = rsn[i & 1][jp];
+                const u32x4_t v = cols8(i, jp);
+                const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+                uint32_t o[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                  const float x0 = rbf(rbf(lo_f(w4[k]) * ss[i]) * lo_f(wv[k]));
+                  const float x1 = rbf(rbf(hi_f(w4[k]) * ss[i]) * hi_f(wv[k]));
+                  o[k] = pack2((x0 * cs[k] - x1 * sn[k]) * osc, (x0 * sn[k] + x1 * cs[k]) * osc);
+                }
+                if (m < M) *(u32x4_t*)(row_ptr(m) + jp * 32) = u32x4_t{o[0], o[1], o[2], o[3]};
+              }
+            }
+            return;
+          }
           if constexpr (NT == 8) {
             // the work-group's 256 RoPE rows (cos | sin, 512 B of fp32 each) staged into the free
             // LDS slots in one round trip by LDS-DMA (32 KiB pieces per wave), chunks XOR-swizzled by
@@ -1784,15 +1824,15 @@ __global__ void __launch_bounds__(256, 1)
 // residual and the 128 KiB of stores) runs while the next tile's operands are already landing,
 // and the next tile starts on fragments in registers instead of on a cold prologue.
 // Row / column offsets of the DMA pieces are those of a full 256-row tile; rows past M or N lie
-// past the buffer descriptor's range and read as zeros (never stored). Not for EPI_QKV_NR (its
-// epilogue stages RoPE rows in the LDS the next tile is landing in).
+// past the buffer descriptor's range and read as zeros (never stored). EPI_QKV_NR takes its RoPE
+// rows straight from the tables here (ring_epilogue's LDS_OK = false): the LDS holds the next tile.
 static int g_cu_count = 0;
 
 template <int EPI, bool I8>
 __global__ void __launch_bounds__(256, 1)
     gemm_w4p_kernel(const char* __restrict__ X, int64_t ldx_b, const char* __restrict__ W, int64_t ldw_b,
                     int M, int N, int K_bytes, EpiArgs e) {
-  static_assert(EPI != EPI_QKV_NR && EPI != EPI_PARTIAL, "w4p epilogues");
+  static_assert(EPI != EPI_PARTIAL, "w4p epilogues");
   using frag = typename MfmaOp<I8>::frag;
   using accT = typename MfmaOp<I8>::acc;
   constexpr int NWAVE = 4, PPO = 8;
@@ -1936,9 +1976,20 @@ __global__ void __launch_bounds__(256, 1)
     ktile(T{}, T{}, T{}, g & 1, cur, 2);
     int kt = 1;
     for (; kt < nk - 2; ++kt) ktile(F{}, T{}, T{}, (g + kt) & 1, cur, kt + 2);
-    ktile(F{}, T{}, T{}, (g + kt) & 1, nxt, 0);      // nk-2: stages the next tile's K tile 0
-    ktile(F{}, T{}, T{}, (g + kt + 1) & 1, nxt, 1);  // nk-1: its K tile 1, reads its set 0
-    ring_epilogue<8, EPI, I8>(acc, e, M, N, cur.m0 + wm * 128, cur.n0 + wn * 128, lane, smem);
+    ktile(F{}, T{}, T{}, (g + kt) & 1, nxt, 0);  // nk-2: stages the next tile's K tile 0
+    if constexpr (EPI != EPI_QKV_NR) {
+      ktile(F{}, T{}, T{}, (g + kt + 1) & 1, nxt, 1);  // nk-1: its K tile 1, reads its set 0
+      ring_epilogue<8, EPI, I8, false>(acc, e, M, N, cur.m0 + wm * 128, cur.n0 + wn * 128, lane, smem);
+    } else {
+      // the norm + RoPE epilogue needs the 64 VGPRs of set 0: read it behind the epilogue (the
+      // wait then also covers the epilogue's stores, issued after K tile 1's pieces)
+      ktile(F{}, T{}, F{}, (g + kt + 1) & 1, nxt, 1);
+      ring_epilogue<8, EPI, I8, false>(acc, e, M, N, cur.m0 + wm * 128, cur.n0 + wn * 128, lane, smem);
+      xa0 ^= (uint32_t)kSlot;
+      wa0 ^= (uint32_t)kSlot;
+      asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+      static_for<0, 16>([&](auto r_t) { rd(I0{}, r_t); });
+    }
     if (!has_next) {
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // no LDS-DMA outlives the work-group
       break;
@@ -2090,6 +2141,13 @@ int launch_splitk(const void* x, int64_t ldx, const void* w, int M, int N, int K
 // 256x256 tiles whenever K spans >= 3 tiles (also the text stream's 2 x 36 tiles: on
 // the side stream its CU-time, not its latency, is what it costs), otherwise the QKV GEMM followed
 // by qie_qk_norm_rope_bf16 on the same rows (the same arithmetic in two launches).
+// 1: the image QKV + norm + RoPE on the persistent gemm_w4p (RoPE rows through registers); 0: on
+// gemm_w4l. Same bits and the same time alone (0.712 vs 0.710 ms), but 1.5 % slower end to end
+// (277.2 vs 272.6 ms per step, same box): the persistent grid holds every CU, so the text stream's
+// QKV waits for all of it and the attention then waits for the text QKV
+#ifndef QIE_NR_W4P
+#define QIE_NR_W4P 0
+#endif
 template <bool I8>
 int launch_qkv_norm_rope(const void* x, int64_t ldx, const void* w, int M, int K, EpiArgs e,
                          const void* nq, const void* nk, const float* cos_tab, const float* sin_tab,
@@ -2113,8 +2171,19 @@ int launch_qkv_norm_rope(const void* x, int64_t ldx, const void* w, int M, int K
     e.rsin = sin_tab;
     e.eps = eps;
     e.qscale = q_scale;
-    // both kernels compute every row bit for bit alike (same K order, same epilogue sums)
-    if (QIE_GEMM_W4 >= 3 && M >= 256 && big_tiles >= 160)
+    // all kernels compute every row bit for bit alike (same K order, same epilogue sums)
+    if (QIE_GEMM_W4 == 4 && QIE_NR_W4P && M >= 256 && big_tiles >= 160) {
+      if (g_cu_count == 0) {
+        int dev = 0, cu = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cu <= 0)
+          cu = 256;
+        g_cu_count = cu;
+      }
+      const int grid = (int)std::min<int64_t>(big_tiles, g_cu_count);
+      gemm_w4p_kernel<EPI_QKV_NR, I8><<<grid, 256, 0, s>>>((const char*)x, ldx * eb, (const char*)w,
+                                                           (int64_t)K * eb, M, N, K * eb, e);
+    } else if (QIE_GEMM_W4 >= 3 && M >= 256 && big_tiles >= 160)
       gemm_w4l_kernel<EPI_QKV_NR, I8><<<(int)big_tiles, 256, 0, s>>>((const char*)x, ldx * eb, (const char*)w,
                                                                     (int64_t)K * eb, M, N, K * eb, e);
     else
