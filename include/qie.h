@@ -324,6 +324,18 @@ int qie_matmul_batched_bf16(const void* x, int64_t ldx, int64_t bsx, const void*
                             int group, const void* bias, void* y, int64_t ldy, int64_t bsy, int M, int N, int K,
                             int batch, int out_f32, qie_stream_t stream);
 
+/* VAE mid-block attention (QwenImageAttentionBlock: one head of C = 384 channels over P latent
+ * pixels; replaces the qie_matmul_f32out_bf16 + qie_softmax_rows_f32_bf16 + P.V chain the
+ * reference's F.scaled_dot_product_attention stands for, diffusers autoencoder_kl_qwenimage [U]):
+ * out[q] = softmax(q . k^T / sqrt(C)) . v for the q / k column blocks of the to_qkv rows
+ * (qkv[p][0..C) and [C..2C), row stride ldqkv) and v given transposed, vt [C][ldvt] with
+ * ldvt >= P rounded up to 32 and ZERO past P. Flash form: fp32 online softmax, scores never
+ * stored; key ranges split over workgroups meet through `workspace` (>=
+ * qie_vae_attention_workspace(P, C) bytes, 16-byte aligned). C must be 384. */
+int qie_vae_attention_bf16(const void* qkv, int64_t ldqkv, const void* vt, int64_t ldvt, int P, int C, void* out,
+                           int64_t ldo, void* workspace, int64_t workspace_bytes, qie_stream_t stream);
+int64_t qie_vae_attention_workspace(int P, int C);
+
 /* y[c][r] = x[r][c] for an R x C bf16 block (row strides ldx, ldy elements). */
 int qie_transpose_bf16(const void* x, int64_t ldx, void* y, int64_t ldy, int R, int C, qie_stream_t stream);
 

@@ -532,6 +532,26 @@ def matmul_heads(x: torch.Tensor, bsx: int, w: torch.Tensor, bsw: int, out: torc
     return out
 
 
+def vae_attention_workspace_bytes(P: int, C: int) -> int:
+    return int(_lib.load().qie_vae_attention_workspace(P, C))
+
+
+def vae_attention(qkv: torch.Tensor, vt: torch.Tensor, out: torch.Tensor, workspace: torch.Tensor) -> torch.Tensor:
+    """Single-head flash attention of the VAE mid-block: ``qkv`` [P, >=3C] bf16 rows (q | k | v),
+    ``vt`` [C, >=roundup(P, 32)] bf16 = v transposed, zero past column P; ``out`` [P, C] bf16
+    (row stride may exceed C); ``workspace`` >= vae_attention_workspace_bytes(P, C) bytes."""
+    _dev(qkv, vt, out, workspace)
+    _chk(qkv.dtype == BF16 and vt.dtype == BF16 and out.dtype == BF16, "bf16 operands")
+    _chk(_is2d_rowmajor(qkv) and _is2d_rowmajor(vt) and _is2d_rowmajor(out), "row-major 2-D views")
+    P = qkv.shape[0]
+    C = vt.shape[0]
+    _chk(qkv.shape[1] >= 3 * C and out.shape == (P, C) and vt.shape[1] >= -(-P // 32) * 32, "vae attention shapes")
+    nbytes = workspace.numel() * workspace.element_size()
+    _lib.call("qie_vae_attention_bf16", _p(qkv), qkv.stride(0), _p(vt), vt.stride(0), P, C, _p(out), out.stride(0),
+              _p(workspace), nbytes, _stream())
+    return out
+
+
 def transpose(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     _dev(x, out)
     _chk(x.dtype == BF16 and _is2d_rowmajor(x), "bf16 row-major")

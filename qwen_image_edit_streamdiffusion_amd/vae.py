@@ -165,7 +165,8 @@ def _convert(sd: Dict[str, torch.Tensor], shapes: Dict[str, Tuple[int, ...]], de
 
 class _VAEBlocks:
     """The resnet / attention blocks both VAE halves share (NHWC, on the workspace buffers
-    "t", "y", "qkv", "s", "p", "vt", "att", "zero_b" and the free activation buffer named)."""
+    "t", "y", "qkv", "vt", "att", the flash-attention workspace "attn_ws" (or, for C != 384, the
+    materialised "s", "p", "zero_b") and the free activation buffer named)."""
 
     w: Dict[str, torch.Tensor]
 
@@ -202,14 +203,17 @@ class _VAEBlocks:
         qkv = ws["qkv"][:P]
         ops.conv2d(t, H, W, wt[f"{prefix}.to_qkv.weight"], wt[f"{prefix}.to_qkv.bias"], ksize=1, out=qkv)
         q, k, v = qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:]
-        s = ws["s"]
-        ops.matmul_f32out(q, k, out=s)
-        p = ws["p"]  # [P, roundup(P, 64)], zero past column P
-        ops.softmax_rows(s, 1.0 / math.sqrt(C), out=p)
         vt = ws["vt"]  # [C, roundup(P, 64)], zero past column P
         ops.transpose(v, out=vt[:, :P])
         att = ws["att"][:P]
-        ops.linear(p, vt, ws["zero_b"][:C], out=att)
+        if "attn_ws" in ws:  # flash form (C = 384, the real model): no score matrix
+            ops.vae_attention(qkv, vt, att, ws["attn_ws"])
+        else:
+            s = ws["s"]
+            ops.matmul_f32out(q, k, out=s)
+            p = ws["p"]  # [P, roundup(P, 64)], zero past column P
+            ops.softmax_rows(s, 1.0 / math.sqrt(C), out=p)
+            ops.linear(p, vt, ws["zero_b"][:C], out=att)
         ops.conv2d(att, H, W, wt[f"{prefix}.proj.weight"], wt[f"{prefix}.proj.bias"], ksize=1, out=x, residual=True)
 
 
@@ -219,9 +223,14 @@ class _VAEBlocks:
         columns from the softmax kernel, zero V^T columns here)."""
         e = dict(dtype=BF16, device=dev)
         kp = -(-P0 // 64) * 64
-        return {"qkv": torch.empty(P0, 3 * C0, **e), "s": torch.empty(P0, P0, dtype=torch.float32, device=dev),
-                "p": torch.empty(P0, kp, **e), "vt": torch.zeros(C0, kp, **e), "att": torch.empty(P0, C0, **e),
-                "zero_b": torch.zeros(C0, **e)}
+        bufs = {"qkv": torch.empty(P0, 3 * C0, **e), "vt": torch.zeros(C0, kp, **e), "att": torch.empty(P0, C0, **e)}
+        if C0 == 384:  # qie_vae_attention_bf16: fp32 partials of the key-range splits only
+            nb = ops.vae_attention_workspace_bytes(P0, C0)
+            bufs["attn_ws"] = torch.empty(-(-nb // 4), dtype=torch.float32, device=dev)
+        else:
+            bufs.update({"s": torch.empty(P0, P0, dtype=torch.float32, device=dev), "p": torch.empty(P0, kp, **e),
+                         "zero_b": torch.zeros(C0, **e)})
+        return bufs
 
 
 class QwenImageVAEDecoder(_VAEBlocks):

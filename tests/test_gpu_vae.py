@@ -131,6 +131,25 @@ def test_vae_rms_norm(dev, C, silu):
     assert torch.equal(z, y)
 
 
+@pytest.mark.parametrize("P", [16384, 1000, 4104])
+def test_vae_attention_flash(dev, P):
+    """qie_vae_attention_bf16 (one head, C = 384) vs fp32 SDPA on the same bf16 q / k / v (torch on
+    the device): rel-L2 <= 4e-3, max |diff| <= 4 bf16 ulps of max|ref| (P rounded to bf16 before
+    P.V, as in the materialised form). 16384: two key ranges; 1000 / 4104: ragged, four ranges."""
+    ops = _ops()
+    C = 384
+    qkv = rnd((P, 3 * C), dev, 1.0, 21)
+    kp = -(-P // 64) * 64
+    vt = torch.zeros(C, kp, dtype=BF16, device=dev)
+    ops.transpose(qkv[:, 2 * C:], out=vt[:, :P])
+    ws = torch.empty(-(-ops.vae_attention_workspace_bytes(P, C) // 4), dtype=torch.float32, device=dev)
+    out = torch.empty(P, C, dtype=BF16, device=dev)
+    ops.vae_attention(qkv, vt, out, ws)
+    q, k, v = (qkv[:, i * C:(i + 1) * C].float() for i in range(3))
+    ref = torch.softmax((q @ k.T) / math.sqrt(C), dim=-1) @ v
+    close(out, ref.to(BF16), ulps=4)
+
+
 def test_softmax_transpose_matmul(dev):
     ops = _ops()
     P, C = 2048, 384
