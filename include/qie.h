@@ -334,7 +334,7 @@ int qie_matmul_batched_bf16(const void* x, int64_t ldx, int64_t bsx, const void*
  * qie_vae_attention_workspace(P, C) bytes, 16-byte aligned). C must be 384. */
 int qie_vae_attention_bf16(const void* qkv, int64_t ldqkv, const void* vt, int64_t ldvt, int P, int C, void* out,
                            int64_t ldo, void* workspace, int64_t workspace_bytes, qie_stream_t stream);
-int64_t qie_vae_attention_workspace(int P, int C);
+int qie_vae_attention_workspace(int P, int C, int64_t* bytes);
 
 /* y[c][r] = x[r][c] for an R x C bf16 block (row strides ldx, ldy elements). */
 int qie_transpose_bf16(const void* x, int64_t ldx, void* y, int64_t ldy, int R, int C, qie_stream_t stream);

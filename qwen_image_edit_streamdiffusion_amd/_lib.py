@@ -72,7 +72,7 @@ SIGNATURES = {
     "qie_softmax_rows_f32_bf16": [P, L, P, L, I, I, F, I, P],
     "qie_transpose_bf16": [P, L, P, L, I, I, P],
     "qie_vae_attention_bf16": [P, L, P, L, I, I, P, L, P, L, P],
-    "qie_vae_attention_workspace": [I, I],
+    "qie_vae_attention_workspace": [I, I, POINTER(c_int64)],
     "qie_vae_rgb_out": [P, L, P, L, P],
     "qie_vae_rgb_in": [P, P, L, P],
     "qie_vae_latents_out_bf16": [P, L, I, I, I, P, P, P, P],
@@ -83,7 +83,7 @@ SIGNATURES = {
     "qie_gelu_erf_bf16": [P, L, I, I, P],
     "qie_silu_mul_bf16": [P, L, I, I, P, L, P],
 }
-_RESTYPES = {"qie_strerror": c_char_p, "qie_vae_attention_workspace": c_int64}
+_RESTYPES = {"qie_strerror": c_char_p}
 
 _lib = None
 

@@ -291,11 +291,16 @@ int va_splits(int P, int& kspan) {
 
 }  // namespace
 
-extern "C" int64_t qie_vae_attention_workspace(int P, int C) {
-  if (P <= 0 || C != kC) return 0;
+static int64_t va_workspace(int P) {
   int kspan;
   const int n = va_splits(P, kspan);
   return (int64_t)n * P * (kC + 2) * 4;
+}
+
+extern "C" int qie_vae_attention_workspace(int P, int C, int64_t* bytes) {
+  QIE_CHECK_ARG(bytes && P > 0 && C == kC);
+  *bytes = va_workspace(P);
+  return QIE_OK;
 }
 
 extern "C" int qie_vae_attention_bf16(const void* qkv, int64_t ldqkv, const void* vt, int64_t ldvt, int P, int C,
@@ -306,7 +311,7 @@ extern "C" int qie_vae_attention_bf16(const void* qkv, int64_t ldqkv, const void
   QIE_CHECK_ARG(((uintptr_t)qkv % 16) == 0 && ((uintptr_t)vt % 16) == 0 && ((uintptr_t)out % 8) == 0 &&
                 ((uintptr_t)workspace % 16) == 0);
   QIE_CHECK_ARG((int64_t)P * ldqkv * 2 < (1ll << 31) && (int64_t)C * ldvt * 2 < (1ll << 31));
-  QIE_CHECK_ARG(workspace_bytes >= qie_vae_attention_workspace(P, C));
+  QIE_CHECK_ARG(workspace_bytes >= va_workspace(P));
   int kspan;
   const int nsplit = va_splits(P, kspan);
   float* opart = (float*)workspace;

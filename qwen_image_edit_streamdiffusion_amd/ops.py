@@ -533,7 +533,9 @@ def matmul_heads(x: torch.Tensor, bsx: int, w: torch.Tensor, bsw: int, out: torc
 
 
 def vae_attention_workspace_bytes(P: int, C: int) -> int:
-    return int(_lib.load().qie_vae_attention_workspace(P, C))
+    n = ctypes.c_int64(0)
+    _lib.call("qie_vae_attention_workspace", P, C, ctypes.byref(n))
+    return int(n.value)
 
 
 def vae_attention(qkv: torch.Tensor, vt: torch.Tensor, out: torch.Tensor, workspace: torch.Tensor) -> torch.Tensor:
