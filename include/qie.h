@@ -286,6 +286,14 @@ int qie_linear_splitk_i8(const void* xq, int64_t ldx, const float* sx, const voi
 int qie_conv2d_bf16(const void* x, int H_in, int W_in, int C, int mode, int ksize, const void* w, int64_t ldw,
                     const void* bias, const void* resid, void* y, int N, qie_stream_t stream);
 
+/* qie_conv2d_bf16 (no residual) followed by QwenImageRMS_norm (+ SiLU when silu != 0) of its output
+ * with `gamma` [N] (the VAE ResidualBlock's conv1 + norm2, rounding points of
+ * qie_vae_rms_norm_bf16): fused into the convolution's epilogue where one wave holds every output
+ * channel of a pixel (N = 96 on the halo-tiled kernel), otherwise the two launches. */
+int qie_conv2d_rmsnorm_bf16(const void* x, int H_in, int W_in, int C, int mode, int ksize, const void* w,
+                            int64_t ldw, const void* bias, const void* gamma, int silu, void* y, int N,
+                            qie_stream_t stream);
+
 /* y[M][N] = x[M][K] . w[N][K]^T as raw fp32 (row strides ldx, ldw elements): attention scores of
  * the VAE mid-block QwenImageAttentionBlock (one head over H*W tokens). K % 64 == 0. */
 int qie_matmul_f32out_bf16(const void* x, int64_t ldx, const void* w, int64_t ldw, float* y, int M, int N,

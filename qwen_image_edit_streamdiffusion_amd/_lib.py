@@ -66,6 +66,7 @@ SIGNATURES = {
     "qie_linear_splitk_bf16": [P, L, P, P, P, I, I, I, I, P, L, P],
     "qie_linear_splitk_i8": [P, L, P, P, P, P, P, I, I, I, I, P, L, P],
     "qie_conv2d_bf16": [P, I, I, I, I, I, P, L, P, P, P, I, P],
+    "qie_conv2d_rmsnorm_bf16": [P, I, I, I, I, I, P, L, P, P, I, P, I, P],
     "qie_matmul_f32out_bf16": [P, L, P, L, P, I, I, I, P],
     "qie_vae_latents_in_bf16": [P, I, I, I, P, P, P, P, P, P],
     "qie_vae_rms_norm_bf16": [P, P, P, L, I, I, P],

@@ -33,7 +33,10 @@ constexpr int kRowBytes = 128;  // one LDS tile row = 64 bf16 or 128 int8 of K
 
 // EPI_QKV_NR: EPI_QKV + the per-head RMSNorm of q and k and their RoPE (gemm_pp only)
 // EPI_RES: out = bf16(out + bf16(acc + bias)) (the VAE ResidualBlock's x + h; conv_kernel only)
-enum Epi { EPI_BIAS = 0, EPI_GELU = 1, EPI_GATE_RES = 2, EPI_QKV = 3, EPI_PARTIAL = 4, EPI_QKV_NR = 5, EPI_RES = 6 };
+// EPI_NORM: out = RMS_norm(bf16(acc + bias)) * gamma (+ SiLU) per pixel over all N channels (the VAE
+// ResidualBlock's norm2 folded into conv1; conv_halo_kernel with one wave across N only)
+enum Epi { EPI_BIAS = 0, EPI_GELU = 1, EPI_GATE_RES = 2, EPI_QKV = 3, EPI_PARTIAL = 4, EPI_QKV_NR = 5, EPI_RES = 6,
+           EPI_NORM = 7 };
 
 struct EpiArgs {
   void* out;          // y / resid / qkv base
@@ -60,6 +63,10 @@ struct EpiArgs {
   // w advancing once per `group` entries (grouped-query attention shares k / v across a group)
   int64_t bsx_b, bsw_b, bso_b;
   int group;
+  // EPI_NORM: per-channel gamma, sqrt(N), SiLU after the norm
+  const bf16_t* ngamma;
+  float nscale;
+  int nsilu;
 };
 
 __device__ __forceinline__ int swz_chunk(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
@@ -2482,10 +2489,12 @@ __global__ void __launch_bounds__(WM * 2 * 64)
 #endif
 constexpr int kConvPD = QIE_HALO_PD, kConvRing = QIE_HALO_PD + 2;
 
-template <int WPX, int MODE>
+template <int WPX, int MODE, int RPW>  // RPW: output rows per wave (4, or 2 for small images)
 struct HaloGeo {
   static constexpr int WN = 4 / WPX;
-  static constexpr int TH = 4 * WPX, NT = 96 * WN;                 // output tile TH x 32 x NT
+  static constexpr int TH = RPW * WPX, NT = 96 * WN;               // output tile TH x 32 x NT
+  static constexpr int NB = 2 * RPW;                               // 16-pixel blocks per wave
+  static constexpr int NF = 6 + NB;                                // fragment reads per step
   static constexpr int HW = MODE == 1 ? 18 : 34;                   // halo columns
   static constexpr int HR = MODE == 1 ? TH / 2 + 2 : TH + 2;       // halo rows
   static constexpr int HPIX = HR * HW;
@@ -2494,7 +2503,8 @@ struct HaloGeo {
   static constexpr int NW = (NT / 16 + 3) / 4;                     // weight pieces per wave
   static constexpr int WBYTES = NW * 4 * 1024;
   static constexpr int LDS = 2 * HBYTES + kConvRing * WBYTES;
-  static constexpr int ROWB = (MODE == 1 ? 2 : 4) * HW * 64;       // halo bytes between waves
+  static constexpr int SRPW = MODE == 1 ? RPW / 2 : RPW;           // halo rows per wave
+  static constexpr int ROWB = SRPW * HW * 64;                      // halo bytes between waves
 };
 
 // s_waitcnt vmcnt(n) + s_barrier: all but the wave's n newest LDS-DMA pieces landed
@@ -2503,12 +2513,12 @@ __device__ __forceinline__ void vm_wait_barrier() {
   static_assert(n >= 0 && n <= 63, "vmcnt");
   asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"i"(n) : "memory");
 }
-template <int EPI, int WPX, int MODE>
+template <int EPI, int WPX, int MODE, int RPW>
 __global__ void __launch_bounds__(256, 1)
     conv_halo_kernel(const bf16_t* __restrict__ X, int H_in, int W_in, int C, int H, int Wd,
                      const char* __restrict__ Wt, int ldw_b, int N, EpiArgs e) {
-  using G = HaloGeo<WPX, MODE>;
-  constexpr int NH = G::NH, NW = G::NW, PD = kConvPD, R = kConvRing;
+  using G = HaloGeo<WPX, MODE, RPW>;
+  constexpr int NH = G::NH, NW = G::NW, PD = kConvPD, R = kConvRing, NB = G::NB;
   __shared__ __attribute__((aligned(16))) char smem_raw[G::LDS];
   char QIE_LDS* smem = (char QIE_LDS*)smem_raw;
 
@@ -2597,7 +2607,7 @@ __global__ void __launch_bounds__(256, 1)
 #pragma unroll
     for (int dx = 0; dx < 3; ++dx) {
       const int q = MODE == 1 ? ((fr + dx - 1) >> 1) + 1 : fr + dx;   // halo column within the block
-      const int hrow2 = (2 * ((MODE == 1 ? 2 : 4) * wp + k)) & 7;     // (2 * absolute halo row) mod 8
+      const int hrow2 = (2 * (G::SRPW * wp + k)) & 7;                 // (2 * absolute halo row) mod 8
       const int col = g ^ ((((hrow2 + q) >> 2) & 1) << 1);
       aoff[k][dx] = (uint32_t)(q * 64 + col * 16);
     }
@@ -2606,9 +2616,9 @@ __global__ void __launch_bounds__(256, 1)
   const uint32_t wbase = (uint32_t)(uintptr_t)wring + wlane;
 
   using acc_t = f32x4_t;
-  acc_t acc[8][6];
+  acc_t acc[NB][6];
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < NB; ++i)
 #pragma unroll
     for (int j = 0; j < 6; ++j) acc[i][j] = acc_t{0, 0, 0, 0};
 
@@ -2616,7 +2626,7 @@ __global__ void __launch_bounds__(256, 1)
   // of the wave, half h). Fragment i of the step (i < 6: weights j = i; then pixel blocks
   // b = i - 6) is one asm ds_read_b128 with its row offset in the offset field; the reads are
   // awaited by the lgkmcnt(0) that opens the step which uses them.
-  auto read_frag = [&](auto t_t, auto i_t, int gc, int s, bf16x8_t (&af)[8], bf16x8_t (&wf)[6]) __attribute__((always_inline)) {
+  auto read_frag = [&](auto t_t, auto i_t, int gc, int s, bf16x8_t (&af)[NB], bf16x8_t (&wf)[6]) __attribute__((always_inline)) {
     constexpr int T = decltype(t_t)::value, dy = T / 3, dx = T % 3, i = decltype(i_t)::value;
     if constexpr (i < 6) {
       const uint32_t pw = wbase + (s % R) * G::WBYTES;
@@ -2629,17 +2639,24 @@ __global__ void __launch_bounds__(256, 1)
       asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(af[b]) : "v"(pa), "i"(imm));
     }
   };
-  auto read_frags = [&](auto t_t, int gc, int s, bf16x8_t (&af)[8], bf16x8_t (&wf)[6]) __attribute__((always_inline)) {
-    static_for<0, 14>([&](auto i_t) __attribute__((always_inline)) { read_frag(t_t, i_t, gc, s, af, wf); });
+  auto read_frags = [&](auto t_t, int gc, int s, bf16x8_t (&af)[NB], bf16x8_t (&wf)[6]) __attribute__((always_inline)) {
+    static_for<0, G::NF>([&](auto i_t) __attribute__((always_inline)) { read_frag(t_t, i_t, gc, s, af, wf); });
   };
   // the step's fragments have landed; every fragment register is redefined behind the wait, so no
   // copy of one can be scheduled above it
-  auto frags_landed = [&](bf16x8_t (&af)[8], bf16x8_t (&wf)[6]) __attribute__((always_inline)) {
-    asm volatile("s_waitcnt lgkmcnt(0)"
-                 : "+v"(af[0]), "+v"(af[1]), "+v"(af[2]), "+v"(af[3]), "+v"(af[4]), "+v"(af[5]), "+v"(af[6]),
-                   "+v"(af[7]), "+v"(wf[0]), "+v"(wf[1]), "+v"(wf[2]), "+v"(wf[3]), "+v"(wf[4]), "+v"(wf[5])
-                 :
-                 : "memory");
+  auto frags_landed = [&](bf16x8_t (&af)[NB], bf16x8_t (&wf)[6]) __attribute__((always_inline)) {
+    if constexpr (NB == 8)
+      asm volatile("s_waitcnt lgkmcnt(0)"
+                   : "+v"(af[0]), "+v"(af[1]), "+v"(af[2]), "+v"(af[3]), "+v"(af[4]), "+v"(af[5]), "+v"(af[6]),
+                     "+v"(af[7]), "+v"(wf[0]), "+v"(wf[1]), "+v"(wf[2]), "+v"(wf[3]), "+v"(wf[4]), "+v"(wf[5])
+                   :
+                   : "memory");
+    else
+      asm volatile("s_waitcnt lgkmcnt(0)"
+                   : "+v"(af[0]), "+v"(af[1]), "+v"(af[2]), "+v"(af[3]), "+v"(wf[0]), "+v"(wf[1]), "+v"(wf[2]),
+                     "+v"(wf[3]), "+v"(wf[4]), "+v"(wf[5])
+                   :
+                   : "memory");
   };
 
   // one step: fragments landed; MFMAs of blocks 0-3 with the step's LDS-DMA pieces (the weights
@@ -2647,8 +2664,9 @@ __global__ void __launch_bounds__(256, 1)
   // for step s + 1; MFMAs of blocks 4-7 with step s + 1's 14 fragment reads one after each of
   // the first 14. Branch-free: past the workgroup's last step the weight pieces, a zero halo and
   // the fragment reads of "step S" still run, into slots no remaining step reads.
-  auto step = [&](auto t_t, int gc, int c, int ti, bf16x8_t (&af)[8], bf16x8_t (&wf)[6], bf16x8_t (&an)[8],
+  auto step = [&](auto t_t, int gc, int c, int ti, bf16x8_t (&af)[NB], bf16x8_t (&wf)[6], bf16x8_t (&an)[NB],
                   bf16x8_t (&wn_)[6]) __attribute__((always_inline)) {
+    constexpr int MF = 3 * NB;  // MFMAs per half step
     constexpr int T = decltype(t_t)::value;
     constexpr bool HALO = T == 1 && !(QIE_HALO_ABL & 2);
     constexpr int NP = ((QIE_HALO_ABL & 1) ? 0 : NW) + (HALO ? NH : 0);
@@ -2662,17 +2680,23 @@ __global__ void __launch_bounds__(256, 1)
     const int gn = gc + 1, cn = c + 1 == NC ? 0 : c + 1;
     char QIE_LDS* const hslot = smem + (gn & 1) * G::HBYTES;
     const int hsoff = __builtin_amdgcn_readfirstlane(cn * 64);
-    static_for<0, 24>([&](auto i_t) __attribute__((always_inline)) {
+    static_assert(NP <= MF, "one LDS-DMA piece per MFMA at most");
+    static_for<0, MF>([&](auto i_t) __attribute__((always_inline)) {
       constexpr int i = decltype(i_t)::value;
       if (!(QIE_HALO_ABL & 4)) Mma4<false>::acc(acc[i / 6][i % 6], wf[i % 6], af[i / 6]);
-      if constexpr (i % 2 == 1 && i / 2 < NP) {
-        constexpr int k = i / 2;
-        if constexpr (!(QIE_HALO_ABL & 1) && k < NW) w4l_dma<0>(wr, wslot + (wave + 4 * k) * 1024, woff[k], wsoff);
-        else {
-          constexpr int kh = (QIE_HALO_ABL & 1) ? k : k - NW;
-          w4l_dma<0>(xr, hslot + (wave * NH + kh) * 1024, hoff[kh], hsoff);
+      // piece k after MFMA 2k + 1 (measured: early beats spread to the end, 5 % at 512^2), or
+      // after MFMA (k + 1) * MF / NP - 1 where the pieces outnumber the odd MFMAs
+      static_for<0, NP>([&](auto k_t) __attribute__((always_inline)) {
+        constexpr int k = decltype(k_t)::value;
+        constexpr int at = 2 * NP <= MF ? 2 * k + 1 : (k + 1) * MF / NP - 1;
+        if constexpr (at == i) {
+          if constexpr (!(QIE_HALO_ABL & 1) && k < NW) w4l_dma<0>(wr, wslot + (wave + 4 * k) * 1024, woff[k], wsoff);
+          else {
+            constexpr int kh = (QIE_HALO_ABL & 1) ? k : k - NW;
+            w4l_dma<0>(xr, hslot + (wave * NH + kh) * 1024, hoff[kh], hsoff);
+          }
         }
-      }
+      });
     });
     if (!(QIE_HALO_ABL & 1)) w_advance();
     // step s + 1's weights landed (PD - 1 later weight steps may stay in flight, plus the next
@@ -2680,15 +2704,15 @@ __global__ void __launch_bounds__(256, 1)
     if constexpr (QIE_HALO_ABL & 3) vm_wait_barrier<0>();
     else if constexpr (T >= 1 && T <= PD) vm_wait_barrier<(PD - 1) * NW + NH>();
     else vm_wait_barrier<(PD - 1) * NW>();
-    static_for<0, 24>([&](auto i_t) __attribute__((always_inline)) {
+    static_for<0, MF>([&](auto i_t) __attribute__((always_inline)) {
       constexpr int i = decltype(i_t)::value;
-      if (!(QIE_HALO_ABL & 4)) Mma4<false>::acc(acc[4 + i / 6][i % 6], wf[i % 6], af[4 + i / 6]);
-      if constexpr (i < 14 && !(QIE_HALO_ABL & 8))
+      if (!(QIE_HALO_ABL & 4)) Mma4<false>::acc(acc[NB / 2 + i / 6][i % 6], wf[i % 6], af[NB / 2 + i / 6]);
+      if constexpr (i < G::NF && !(QIE_HALO_ABL & 8))
         read_frag(std::integral_constant<int, (T + 1) % 9>{}, i_t, T == 8 ? gc + 1 : gc, s + 1, an, wn_);
     });
     if constexpr (QIE_HALO_ABL & 8) {
 #pragma unroll
-      for (int b = 0; b < 8; ++b) an[b] = af[b];
+      for (int b = 0; b < NB; ++b) an[b] = af[b];
 #pragma unroll
       for (int j = 0; j < 6; ++j) wn_[j] = wf[j];
     }
@@ -2701,29 +2725,70 @@ __global__ void __launch_bounds__(256, 1)
     // inline-asm MFMAs), then redefine the accumulators so no read is hoisted above the wait
     asm volatile("s_nop 15\n\ts_nop 7" ::: "memory");
 #pragma unroll
-    for (int b = 0; b < 8; ++b)
+    for (int b = 0; b < NB; ++b)
       asm volatile("" : "+a"(acc[b][0]), "+a"(acc[b][1]), "+a"(acc[b][2]), "+a"(acc[b][3]), "+a"(acc[b][4]),
                    "+a"(acc[b][5]));
     const int nb = n0 + wn * 96 + g * 4;
     u32x2_t bw[6];
 #pragma unroll
     for (int j = 0; j < 6; ++j) bw[j] = *(const u32x2_t*)(e.bias + nb + j * 16);
-    int mrow[8];
+    int mrow[NB];
 #pragma unroll
-    for (int b = 0; b < 8; ++b) {
-      const int y = y0 + 4 * wp + (b >> 1), x = x0 + 16 * (b & 1) + fr;
+    for (int b = 0; b < NB; ++b) {
+      const int y = y0 + RPW * wp + (b >> 1), x = x0 + 16 * (b & 1) + fr;
       mrow[b] = (y < H && x < Wd) ? y * Wd + x : -1;
     }
-    u32x2_t xw[8][6];
+    if constexpr (EPI == EPI_NORM) {
+      static_assert(G::WN == 1, "the norm needs every channel of a pixel in one wave");
+      // QwenImageRMS_norm of vae.hip's rms_norm_kernel on the rounded conv output: the pixel's 96
+      // channels sit in its 4 lanes g (24 each), the sum of squares meets by two xor shuffles
+      u32x2_t gw[6];
+#pragma unroll
+      for (int j = 0; j < 6; ++j) gw[j] = *(const u32x2_t*)(e.ngamma + nb + j * 16);
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        float v[6][4];
+        float ss = 0.f;
+#pragma unroll
+        for (int j = 0; j < 6; ++j) {
+          v[j][0] = acc[b][j][0] + lo_f(bw[j].x);
+          v[j][1] = acc[b][j][1] + hi_f(bw[j].x);
+          v[j][2] = acc[b][j][2] + lo_f(bw[j].y);
+          v[j][3] = acc[b][j][3] + hi_f(bw[j].y);
+          rbf2(v[j][0], v[j][1]);
+          rbf2(v[j][2], v[j][3]);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) ss = __builtin_fmaf(v[j][r], v[j][r], ss);
+        }
+        ss += __shfl_xor(ss, 16, 64);
+        ss += __shfl_xor(ss, 32, 64);
+        const float d = fmaxf(rbf(sqrtf(ss)), 1e-12f);
+#pragma unroll
+        for (int j = 0; j < 6; ++j) {
+          const float gg[4] = {lo_f(gw[j].x), hi_f(gw[j].x), lo_f(gw[j].y), hi_f(gw[j].y)};
+          float u[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            u[r] = rbf(rbf(rbf(v[j][r] / d) * e.nscale) * gg[r]);
+            if (e.nsilu) u[r] = u[r] * __builtin_amdgcn_rcpf(1.0f + __expf(-u[r]));
+          }
+          if (mrow[b] >= 0)
+            *(u32x2_t*)((bf16_t*)e.out + (int64_t)mrow[b] * e.ldo + nb + j * 16) = u32x2_t{pack2(u[0], u[1]), pack2(u[2], u[3])};
+          acc[b][j] = acc_t{0, 0, 0, 0};
+        }
+      }
+      return;
+    }
+    u32x2_t xw[NB][6];
     if constexpr (EPI == EPI_RES) {
 #pragma unroll
-      for (int b = 0; b < 8; ++b)
+      for (int b = 0; b < NB; ++b)
 #pragma unroll
         for (int j = 0; j < 6; ++j)
           xw[b][j] = *(const u32x2_t*)((const bf16_t*)e.out + (int64_t)max(mrow[b], 0) * e.ldo + nb + j * 16);
     }
 #pragma unroll
-    for (int b = 0; b < 8; ++b) {
+    for (int b = 0; b < NB; ++b) {
 #pragma unroll
       for (int j = 0; j < 6; ++j) {
         float v[4] = {acc[b][j][0] + lo_f(bw[j].x), acc[b][j][1] + hi_f(bw[j].x), acc[b][j][2] + lo_f(bw[j].y),
@@ -2749,7 +2814,7 @@ __global__ void __launch_bounds__(256, 1)
 #pragma unroll
   for (int s = 0; s < PD; ++s) dma_w(s);
   vm_wait_barrier<(PD - 1) * NW>();
-  bf16x8_t a0[8], w0[6], a1[8], w1[6];
+  bf16x8_t a0[NB], w0[6], a1[NB], w1[6];
   read_frags(std::integral_constant<int, 0>{}, 0, 0, a0, w0);
   int cx0, cy0, cn0, ti = 0, c = 0;
   tile_of(0, cx0, cy0, cn0);
@@ -2961,9 +3026,35 @@ extern "C" int qie_linear_splitk_i8(const void* xq, int64_t ldx, const float* sx
 }
 
 // ---------------------------------------------------------------------------- VAE convolutions
+static int conv2d_impl(const void* x, int H_in, int W_in, int C, int mode, int ksize, const void* w, int64_t ldw,
+                       const void* bias, const void* resid, void* y, int N, const void* ngamma, int nsilu,
+                       qie_stream_t stream);
+
 extern "C" int qie_conv2d_bf16(const void* x, int H_in, int W_in, int C, int mode, int ksize, const void* w,
                                int64_t ldw, const void* bias, const void* resid, void* y, int N,
                                qie_stream_t stream) {
+  return conv2d_impl(x, H_in, W_in, C, mode, ksize, w, ldw, bias, resid, y, N, nullptr, 0, stream);
+}
+
+// conv + QwenImageRMS_norm (+ SiLU) of its output (the ResidualBlock's conv1 + norm2): one launch
+// where the halo kernel holds every output channel of a pixel in one wave (N = 96), otherwise the
+// conv and qie_vae_rms_norm_bf16 in place
+extern "C" int qie_conv2d_rmsnorm_bf16(const void* x, int H_in, int W_in, int C, int mode, int ksize, const void* w,
+                                       int64_t ldw, const void* bias, const void* gamma, int silu, void* y, int N,
+                                       qie_stream_t stream) {
+  QIE_CHECK_ARG(gamma && ((uintptr_t)gamma % 16) == 0);
+  const int rc = conv2d_impl(x, H_in, W_in, C, mode, ksize, w, ldw, bias, nullptr, y, N, gamma, silu, stream);
+  if (rc != QIE_ERR_UNSUPPORTED) return rc;
+  const int rc2 = conv2d_impl(x, H_in, W_in, C, mode, ksize, w, ldw, bias, nullptr, y, N, nullptr, 0, stream);
+  if (rc2) return rc2;
+  const int64_t P = (int64_t)(mode == 1 ? 2 * H_in : mode == 2 ? H_in / 2 : H_in) *
+                    (mode == 1 ? 2 * W_in : mode == 2 ? W_in / 2 : W_in);
+  return qie_vae_rms_norm_bf16(y, gamma, y, P, N, silu, stream);
+}
+
+static int conv2d_impl(const void* x, int H_in, int W_in, int C, int mode, int ksize, const void* w, int64_t ldw,
+                       const void* bias, const void* resid, void* y, int N, const void* ngamma, int nsilu,
+                       qie_stream_t stream) {
   QIE_CHECK_ARG(x && w && bias && y && H_in > 0 && W_in > 0 && C > 0 && C % 8 == 0);
   QIE_CHECK_ARG(mode >= 0 && mode <= 2 && (ksize == 1 || ksize == 3) && N > 0 && N % 4 == 0);
   QIE_CHECK_ARG(mode != 2 || (ksize == 3 && H_in % 2 == 0 && W_in % 2 == 0));
@@ -2979,13 +3070,21 @@ extern "C" int qie_conv2d_bf16(const void* x, int H_in, int W_in, int C, int mod
   const hipStream_t s = (hipStream_t)stream;
   QIE_CHECK_ARG(!resid || resid == y);  // y = bf16(resid + bf16(acc + bias)), in place
   EpiArgs e = make_epi(y, N, bias);
+  e.ngamma = (const bf16_t*)ngamma;
+  e.nscale = sqrtf((float)N);
+  e.nsilu = nsilu;
   const char* wc = (const char*)w;
 #if QIE_CONV_HALO
   // halo-tiled kernel: 3x3, same size or upsampled, 32-channel chunks, 96 / 192-channel tiles,
   // enough tiles to fill the chip (smaller grids stay on conv_kernel's 128-pixel tiles)
   if (ksize == 3 && mode != 2 && C % 32 == 0 && (N == 96 || N % 192 == 0) && (int64_t)N * ldw * 2 < (1ll << 31)) {
-    const int wpx = N == 96 ? 4 : 2, th = 4 * wpx, nt = N == 96 ? 96 : 192;
-    const int64_t nwg = (int64_t)((c.W_out + 31) / 32) * ((c.H_out + th - 1) / th) * (N / nt);
+    const int wpx = N == 96 ? 4 : 2, nt = N == 96 ? 96 : 192;
+    auto tiles = [&](int rpw) {
+      return (int64_t)((c.W_out + 31) / 32) * ((c.H_out + rpw * wpx - 1) / (rpw * wpx)) * (N / nt);
+    };
+    // 4 output rows per wave; 2 where that leaves too few tiles for the chip (128^2 x 384)
+    const int rpw = tiles(4) >= QIE_CONV_HALO_MIN ? 4 : 2;
+    const int64_t nwg = tiles(rpw);
     if (nwg >= QIE_CONV_HALO_MIN) {
       const bf16_t* xb = (const bf16_t*)x;
       if (g_cu_count == 0) {
@@ -2998,7 +3097,10 @@ extern "C" int qie_conv2d_bf16(const void* x, int H_in, int W_in, int C, int mod
       const int grid = QIE_HALO_PERSIST ? (int)std::min<int64_t>(nwg, g_cu_count) : (int)nwg;
       auto k = [&](auto epi_t, auto wpx_t, auto mode_t) {
         constexpr int EP = decltype(epi_t)::value, WX = decltype(wpx_t)::value, MD = decltype(mode_t)::value;
-        conv_halo_kernel<EP, WX, MD><<<grid, 256, 0, s>>>(xb, H_in, W_in, C, c.H_out, c.W_out, wc, (int)(ldw * 2), N, e);
+        if (rpw == 4)
+          conv_halo_kernel<EP, WX, MD, 4><<<grid, 256, 0, s>>>(xb, H_in, W_in, C, c.H_out, c.W_out, wc, (int)(ldw * 2), N, e);
+        else
+          conv_halo_kernel<EP, WX, MD, 2><<<grid, 256, 0, s>>>(xb, H_in, W_in, C, c.H_out, c.W_out, wc, (int)(ldw * 2), N, e);
       };
       auto by_mode = [&](auto epi_t, auto wpx_t) {
         if (mode == 1) k(epi_t, wpx_t, std::integral_constant<int, 1>{});
@@ -3008,14 +3110,21 @@ extern "C" int qie_conv2d_bf16(const void* x, int H_in, int W_in, int C, int mod
         if (wpx == 4) by_mode(epi_t, std::integral_constant<int, 4>{});
         else by_mode(epi_t, std::integral_constant<int, 2>{});
       };
-      if (resid) by_wpx(std::integral_constant<int, EPI_RES>{});
-      else by_wpx(std::integral_constant<int, EPI_BIAS>{});
+      if (ngamma) {
+        if (wpx != 4) return QIE_ERR_UNSUPPORTED;
+        by_mode(std::integral_constant<int, EPI_NORM>{}, std::integral_constant<int, 4>{});
+      } else if (resid) {
+        by_wpx(std::integral_constant<int, EPI_RES>{});
+      } else {
+        by_wpx(std::integral_constant<int, EPI_BIAS>{});
+      }
       return qie_last_error();
     }
   }
 #endif
   // 128-pixel tiles (4 waves, 2 workgroups per CU; 256-pixel / 8-wave tiles from QIE_CONV_BIG_MIN
   // workgroups); 96-wide output tiles when N is a multiple of 96 but not of 128 (96, 192)
+  if (ngamma) return QIE_ERR_UNSUPPORTED;  // the caller runs the conv, then the norm
   const bool n96 = N % 128 != 0 && N % 96 == 0;
   const int bn = n96 ? 96 : 128;
   const int tn = (N + bn - 1) / bn;

@@ -462,6 +462,26 @@ def conv2d(x: torch.Tensor, H: int, W: int, w: torch.Tensor, b: torch.Tensor, ks
     return out
 
 
+def conv2d_rmsnorm(x: torch.Tensor, H: int, W: int, w: torch.Tensor, b: torch.Tensor, gamma: torch.Tensor,
+                   silu: bool, ksize: int = 3, up: bool = False, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """conv2d (no residual) then vae_rms_norm(+SiLU) of its output with ``gamma`` [N], in one launch
+    where the kernel allows (qie_conv2d_rmsnorm_bf16)."""
+    _dev(x, w, b, gamma, out)
+    _chk(x.dtype == BF16 and w.dtype == BF16 and b.dtype == BF16 and gamma.dtype == BF16, "bf16 operands required")
+    _chk(x.dim() == 2 and x.is_contiguous() and x.shape[0] == H * W, "x: [H*W, C] contiguous")
+    C = x.shape[1]
+    N = w.shape[0]
+    _chk(C % 8 == 0 and N % 4 == 0 and w.is_contiguous() and w.shape[1] >= conv_kpad(C, ksize), "conv shapes")
+    _chk(b.numel() == N and gamma.numel() == N and gamma.is_contiguous(), "bias / gamma")
+    P = H * W * 4 if up else H * W
+    if out is None:
+        out = torch.empty(P, N, dtype=BF16, device=x.device)
+    _chk(out.shape == (P, N) and out.is_contiguous() and out.dtype == BF16, "out [P, N]")
+    _lib.call("qie_conv2d_rmsnorm_bf16", _p(x), H, W, C, 1 if up else 0, ksize, _p(w), w.stride(0), _p(b), _p(gamma),
+              int(silu), _p(out), N, _stream())
+    return out
+
+
 def matmul_f32out(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Raw fp32 x @ w.T for bf16 row-major views (row strides may exceed K)."""
     _dev(x, w, out)

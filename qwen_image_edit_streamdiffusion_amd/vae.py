@@ -182,8 +182,8 @@ class _VAEBlocks:
         t = self._view(ws["t"], P, a)
         ops.vae_rms_norm(x, wt[f"{prefix}.norm1.gamma"], True, out=t)
         y = self._view(ws["y"], P, b)
-        ops.conv2d(t, H, W, wt[f"{prefix}.conv1.weight"], wt[f"{prefix}.conv1.bias"], out=y)
-        ops.vae_rms_norm(y, wt[f"{prefix}.norm2.gamma"], True, out=y)
+        ops.conv2d_rmsnorm(t, H, W, wt[f"{prefix}.conv1.weight"], wt[f"{prefix}.conv1.bias"],
+                           wt[f"{prefix}.norm2.gamma"], True, out=y)  # conv1 + norm2 (+ SiLU)
         if a != b:  # shortcut into a free buffer; conv2 adds onto it
             name = free[0]
             h = self._view(ws[name], P, b)

@@ -97,6 +97,35 @@ def test_conv2d_residual_halo(dev):
         close(out, _nhwc(ref), ulps=4)
 
 
+@pytest.mark.parametrize("H,W,C,N,up", [
+    (512, 256, 96, 96, False),   # halo kernel, N = 96: norm fused into the epilogue
+    (256, 256, 192, 96, True),   # fused, upsampled halo
+    (64, 64, 96, 96, False),     # too few tiles: conv_kernel, then the norm kernel
+    (128, 256, 96, 192, False),  # N = 192 (channels over two waves): two launches
+])
+def test_conv2d_rmsnorm(dev, H, W, C, N, up):
+    """conv1 + norm2 (+ SiLU) of the ResidualBlock in one call == the conv then qie_vae_rms_norm_bf16
+    (the fused sum of squares runs in another order: within 1 bf16 ulp), and both vs the fp32
+    reference chain."""
+    from qwen_image_edit_streamdiffusion_amd.vae import conv_weight
+    ops = _ops()
+    x = rnd((C, H, W), dev, 1.0, 31)
+    w4 = rnd((N, C, 3, 3), dev, 1.0 / math.sqrt(9 * C), 32)
+    b = rnd((N,), dev, 0.1, 33)
+    gamma = (1 + rnd((N,), dev, 0.1, 34).float()).to(BF16)
+    fused = ops.conv2d_rmsnorm(_nhwc(x), H, W, conv_weight(w4), b, gamma, True, up=up)
+    two = ops.conv2d(_nhwc(x), H, W, conv_weight(w4), b, up=up)
+    ops.vae_rms_norm(two, gamma, True, out=two)
+    close(fused, two, ulps=2)
+    xi = x.float().cpu()[None]
+    if up:
+        xi = F.interpolate(xi, scale_factor=2.0, mode="nearest-exact")
+    conv = F.conv2d(xi, w4.float().cpu(), b.float().cpu(), padding=1)[0].to(BF16).float()
+    r = V._R(True)
+    ref = V.silu(V.rms_norm(conv[None], gamma.float().cpu().view(N, 1, 1), r), r)[0]
+    close(fused, _nhwc(ref.to(BF16)), rel_l2=8e-3, ulps=8)
+
+
 def test_conv2d_residual_and_causal3d(dev):
     """A causal 3x3x3 conv on one frame (oracle: F.pad 2 zero frames + conv3d) == the 2-D conv with
     the last temporal slice, and the residual epilogue adds onto the shortcut in place."""
