@@ -1833,6 +1833,9 @@ __global__ void __launch_bounds__(256, 1)
 // Row / column offsets of the DMA pieces are those of a full 256-row tile; rows past M or N lie
 // past the buffer descriptor's range and read as zeros (never stored). EPI_QKV_NR takes its RoPE
 // rows straight from the tables here (ring_epilogue's LDS_OK = false): the LDS holds the next tile.
+#ifndef QIE_W4P_GROUP  // 0: by output width (below); else a fixed group size
+#define QIE_W4P_GROUP 0
+#endif
 static int g_cu_count = 0;
 
 template <int EPI, bool I8>
@@ -1859,7 +1862,9 @@ __global__ void __launch_bounds__(256, 1)
   };
   auto tile_of = [&](int vb) {
     const int wgid = xcd_remap(vb, nwg);
-    constexpr int GROUP = 8;
+    // M tiles per group of the tile order: 4 for the narrow outputs (N = 3072: down-proj 0.855 ->
+    // 0.838 ms, out-proj equal), 8 for the wide ones (up / QKV: 8 best by 0.5-1 %)
+    const int GROUP = QIE_W4P_GROUP ? QIE_W4P_GROUP : (tiles_n <= 16 ? 4 : 8);
     const int per_group = GROUP * tiles_n;
     const int first_m = (wgid / per_group) * GROUP;
     const int gsz = min(tiles_m - first_m, GROUP);
