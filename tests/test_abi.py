@@ -91,3 +91,14 @@ def test_invalid_arguments_rejected_on_host(lib):
     assert lib.qie_attention_workspace_bytes(1, 1, 256, 200, 0, None) == -1
     kv = (ctypes.c_int * 1)(512)
     assert lib.qie_attention_fwd_split_bf16(16, 1, 1, 512, kv, 16, None, 512, 0, 0.1, None, 0, None) == -1
+    # VAE flash attention: workspace query (host only), C must be 384, vt wide enough, workspace size
+    assert lib.qie_vae_attention_workspace(16384, 384, ctypes.byref(n)) == 0
+    assert n.value == 2 * 16384 * 386 * 4  # two key ranges of fp32 partials at 128 query blocks
+    assert lib.qie_vae_attention_workspace(16384, 256, ctypes.byref(n)) == -1
+    assert lib.qie_vae_attention_bf16(16, 1152, 16, 16384, 16384, 256, 16, 384, 16, 1 << 30, None) == -1
+    assert lib.qie_vae_attention_bf16(16, 1152, 16, 100, 16384, 384, 16, 384, 16, 1 << 30, None) == -1
+    assert lib.qie_vae_attention_bf16(16, 1152, 16, 16384, 16384, 384, 16, 384, 16, 1024, None) == -1
+    # fused conv + RMS-norm: gamma required (and 16-byte aligned); the conv's own checks apply
+    assert lib.qie_conv2d_rmsnorm_bf16(16, 64, 64, 96, 0, 3, 16, 896, 16, None, 1, 16, 96, None) == -1
+    assert lib.qie_conv2d_rmsnorm_bf16(16, 64, 64, 96, 0, 3, 16, 896, 16, 18, 1, 16, 96, None) == -1
+    assert lib.qie_conv2d_rmsnorm_bf16(16, 64, 64, 92, 0, 3, 16, 896, 16, 16, 1, 16, 96, None) == -1
