@@ -70,6 +70,9 @@ constexpr int kRing = 3;
 #ifndef QIE_ATTN_VPRIO  // ... and in its softmax phase
 #define QIE_ATTN_VPRIO 0
 #endif
+#ifndef QIE_ATTN_STATIC  // >= 0: waves 4-7 at this priority for the whole loop, no per-phase flips
+#define QIE_ATTN_STATIC -1
+#endif
 #ifndef QIE_ATTN_ONES  // 1: row sums by 4 MFMAs against a ones operand in the MFMA phase (log2q path)
 #define QIE_ATTN_ONES 0
 #endif
@@ -279,7 +282,7 @@ __global__ void __launch_bounds__(512) attn_pp_kernel(AttnArgs a) {
     bf16x8_t A[8];
     // the MFMA wave outranks its SIMD partner (in its softmax phase) for issue: otherwise the
     // older wave group wins arbitration and starves the younger group's MFMA phase
-    __builtin_amdgcn_s_setprio(QIE_ATTN_MPRIO);
+    if (QIE_ATTN_STATIC < 0) __builtin_amdgcn_s_setprio(QIE_ATTN_MPRIO);
 #pragma unroll
     for (int i = i0; i < i0 + PF && i < i1; ++i) A[i & 7] = opA(i, tk, tv);
 #pragma unroll
@@ -290,7 +293,7 @@ __global__ void __launch_bounds__(512) attn_pp_kernel(AttnArgs a) {
         if (i >= 16 && ((i - 16) & 3) == 3) mma32(st.lsum, ones, st.pf[(i - 16) >> 2]);
       }
     }
-    __builtin_amdgcn_s_setprio(QIE_ATTN_VPRIO);
+    if (QIE_ATTN_STATIC < 0) __builtin_amdgcn_s_setprio(QIE_ATTN_VPRIO);
   };
   // V-phase: softmax of S(t) into P(t), DMA of later tiles; ends with the phase barrier
   auto vphase = [&](int t) {
@@ -423,6 +426,9 @@ __global__ void __launch_bounds__(512) attn_pp_kernel(AttnArgs a) {
   __builtin_amdgcn_s_waitcnt(0);                     // Q fragments (hipcc-tracked)
   asm volatile("s_barrier" ::: "memory");
   if (grp == 1) asm volatile("s_barrier" ::: "memory");
+  // static form (MI355X_MICROARCH.md "Two waves per SIMD" item 4): one priority per wave group
+  // for the whole loop instead of per-phase flips
+  if (QIE_ATTN_STATIC >= 0 && grp == 1) __builtin_amdgcn_s_setprio(QIE_ATTN_STATIC);
 #pragma unroll
   for (int db = 0; db < 4; ++db) st.o[db] = f32x16_t{};
   st.m_run = PRE ? 0.f : -INFINITY;  // PRE: finite (it is the MFMA's C); tile t0 sets it
