@@ -2743,6 +2743,20 @@ __global__ void __launch_bounds__(256, 1)
       const int y = y0 + RPW * wp + (b >> 1), x = x0 + 16 * (b & 1) + fr;
       mrow[b] = (y < H && x < Wd) ? y * Wd + x : -1;
     }
+    // the block's 6 packed 4-channel pieces, widened to 16-byte stores: one v_permlane16_swap per
+    // dword between tiles j and j + 1 leaves each lane 8 consecutive channels of its pixel
+    // (g = 0: channels 0-7 of the 32, 1: 16-23, 2: 8-15, 3: 24-31)
+    const int dl = (g & 1) * 16 + (g >> 1) * 8;
+    auto store_row = [&](int b, const u32x2_t (&pk)[6]) __attribute__((always_inline)) {
+#pragma unroll
+      for (int jp = 0; jp < 3; ++jp) {
+        const auto sx = __builtin_amdgcn_permlane16_swap(pk[2 * jp].x, pk[2 * jp + 1].x, false, false);
+        const auto sy = __builtin_amdgcn_permlane16_swap(pk[2 * jp].y, pk[2 * jp + 1].y, false, false);
+        if (mrow[b] >= 0)
+          *(u32x4_t*)((bf16_t*)e.out + (int64_t)mrow[b] * e.ldo + n0 + wn * 96 + jp * 32 + dl) =
+              u32x4_t{sx[0], sy[0], sx[1], sy[1]};
+      }
+    };
     if constexpr (EPI == EPI_NORM) {
       static_assert(G::WN == 1, "the norm needs every channel of a pixel in one wave");
       // QwenImageRMS_norm of vae.hip's rms_norm_kernel on the rounded conv output: the pixel's 96
@@ -2753,6 +2767,7 @@ __global__ void __launch_bounds__(256, 1)
 #pragma unroll
       for (int b = 0; b < NB; ++b) {
         float v[6][4];
+        u32x2_t pk[6];
         float ss = 0.f;
 #pragma unroll
         for (int j = 0; j < 6; ++j) {
@@ -2777,10 +2792,10 @@ __global__ void __launch_bounds__(256, 1)
             u[r] = rbf(rbf(rbf(v[j][r] / d) * e.nscale) * gg[r]);
             if (e.nsilu) u[r] = u[r] * __builtin_amdgcn_rcpf(1.0f + __expf(-u[r]));
           }
-          if (mrow[b] >= 0)
-            *(u32x2_t*)((bf16_t*)e.out + (int64_t)mrow[b] * e.ldo + nb + j * 16) = u32x2_t{pack2(u[0], u[1]), pack2(u[2], u[3])};
+          pk[j] = u32x2_t{pack2(u[0], u[1]), pack2(u[2], u[3])};
           acc[b][j] = acc_t{0, 0, 0, 0};
         }
+        store_row(b, pk);
       }
       return;
     }
@@ -2794,6 +2809,7 @@ __global__ void __launch_bounds__(256, 1)
     }
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
+      u32x2_t pk[6];
 #pragma unroll
       for (int j = 0; j < 6; ++j) {
         float v[4] = {acc[b][j][0] + lo_f(bw[j].x), acc[b][j][1] + hi_f(bw[j].x), acc[b][j][2] + lo_f(bw[j].y),
@@ -2806,10 +2822,10 @@ __global__ void __launch_bounds__(256, 1)
           v[2] += lo_f(xw[b][j].y);
           v[3] += hi_f(xw[b][j].y);
         }
-        if (mrow[b] >= 0)
-          *(u32x2_t*)((bf16_t*)e.out + (int64_t)mrow[b] * e.ldo + nb + j * 16) = u32x2_t{pack2(v[0], v[1]), pack2(v[2], v[3])};
+        pk[j] = u32x2_t{pack2(v[0], v[1]), pack2(v[2], v[3])};
         acc[b][j] = acc_t{0, 0, 0, 0};
       }
+      store_row(b, pk);
     }
   };
 
