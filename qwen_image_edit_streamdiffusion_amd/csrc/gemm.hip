@@ -2486,6 +2486,9 @@ __global__ void __launch_bounds__(WM * 2 * 64)
 #ifndef QIE_HALO_PD  // weight prefetch distance (steps); the ring has PD + 2 slots
 #define QIE_HALO_PD 4
 #endif
+#ifndef QIE_CONV_NORM_FUSE  // 1: qie_conv2d_rmsnorm_bf16 folds the norm into the halo epilogue
+#define QIE_CONV_NORM_FUSE 1
+#endif
 #ifndef QIE_HALO_PERSIST  // 1: one workgroup per CU walking its tiles; 0: one workgroup per tile
 #define QIE_HALO_PERSIST 1
 #endif
@@ -2783,13 +2786,18 @@ __global__ void __launch_bounds__(256, 1)
         ss += __shfl_xor(ss, 16, 64);
         ss += __shfl_xor(ss, 32, 64);
         const float d = fmaxf(rbf(sqrtf(ss)), 1e-12f);
+        // v / d correctly rounded from one reciprocal: q = v * (1/d), then one residual step
+        // q + (v - q d) / d (exact for these normal-range operands, 3 VALU instead of ~10 per value)
+        const float rd = __builtin_amdgcn_rcpf(d);
 #pragma unroll
         for (int j = 0; j < 6; ++j) {
           const float gg[4] = {lo_f(gw[j].x), hi_f(gw[j].x), lo_f(gw[j].y), hi_f(gw[j].y)};
           float u[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            u[r] = rbf(rbf(rbf(v[j][r] / d) * e.nscale) * gg[r]);
+            const float q0 = v[j][r] * rd;
+            const float q = __builtin_fmaf(__builtin_fmaf(-q0, d, v[j][r]), rd, q0);
+            u[r] = rbf(rbf(rbf(q) * e.nscale) * gg[r]);
             if (e.nsilu) u[r] = u[r] * __builtin_amdgcn_rcpf(1.0f + __expf(-u[r]));
           }
           pk[j] = u32x2_t{pack2(u[0], u[1]), pack2(u[2], u[3])};
@@ -3132,7 +3140,7 @@ static int conv2d_impl(const void* x, int H_in, int W_in, int C, int mode, int k
         else by_mode(epi_t, std::integral_constant<int, 2>{});
       };
       if (ngamma) {
-        if (wpx != 4) return QIE_ERR_UNSUPPORTED;
+        if (wpx != 4 || !QIE_CONV_NORM_FUSE) return QIE_ERR_UNSUPPORTED;
         by_mode(std::integral_constant<int, EPI_NORM>{}, std::integral_constant<int, 4>{});
       } else if (resid) {
         by_wpx(std::integral_constant<int, EPI_RES>{});
