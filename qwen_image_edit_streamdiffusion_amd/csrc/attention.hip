@@ -506,6 +506,354 @@ __global__ void __launch_bounds__(512) attn_pp_kernel(AttnArgs a) {
   }
 }
 
+// =============================================================================================
+// attn16_kernel: the log2-q (PRE) attention on v_mfma_f32_16x16x32_bf16. Same work-group shape,
+// K / V rings, LDS-DMA, two-group ping-pong and barriers as attn_pp_kernel; only the MFMA shape
+// changes. MI355X_MICROARCH.md "DVFS give-back" (7): on random data the chip holds a higher
+// clock under 16x16x32 loops than under 32x32x16 ones (~1.12-1.15x FLOP/s at equal cycles per
+// FLOP), and this kernel is MFMA-paced.
+// Per wave: 32 query rows = two 16-row column blocks qb; per 64-key tile four 16-key blocks kb.
+// Lane (g = lane >> 4, c = lane & 15):
+//   S^T[kb][qb] (16 keys x 16 queries, f32x4): query qb*16 + c, keys kb*16 + 4g + r (r = 0..3)
+//     = sum_ks K[kb*16 + c][32ks + 8g ..] (A, ds_read_b128) x Q^T (B, registers qf[qb][ks])
+//   -> the lane's 16 scores of a query are reduced over the 4 lane groups by two swaps
+//   P^T B operand of key step ks2 (32 keys): elements 0..3 = kb 2ks2, 4..7 = kb 2ks2 + 1, so the
+//   k index 8g + j maps to key 32ks2 + 4g + j (j < 4) / 32ks2 + 16 + 4g + (j - 4)
+//   O^T[db][qb] (f32x4): d = 16db + 4g + r of query qb*16 + c
+//     += V^T (A: two ds_read_b64_tr_b16 of 4 keys x 16 d each, keys as the P^T permutation) x P^T
+// V ring swizzle: chunk ^ ((row & 3) << 2) ^ (((row >> 2) & 1) << 1), so both 16-lane groups of a
+// transposed read's 32-lane half (rows 4 apart) hit distinct banks.
+#ifndef QIE_ATTN16
+#define QIE_ATTN16 0  // 1: log2-q launches on attn16_kernel (measured 1.5-3 % slower, off)
+#endif
+#ifndef QIE_ATTN16_PF
+#define QIE_ATTN16_PF 4  // operand prefetch distance in fragments (2 MFMAs each)
+#endif
+
+__device__ __forceinline__ void mma16(f32x4_t& c, const bf16x8_t& a, const bf16x8_t& b) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(c) : "v"(a), "v"(b));
+}
+__device__ __forceinline__ void mma16_c(f32x4_t& c, const bf16x8_t& a, const bf16x8_t& b, const f32x4_t& c0) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %3" : "=&v"(c) : "v"(a), "v"(b), "v"(c0));
+}
+__device__ __forceinline__ float max_over_groups(float m) {  // max over lanes c, c+16, c+32, c+48
+  const auto s16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(m), __float_as_uint(m), false, false);
+  m = fmaxf(__uint_as_float(s16[0]), __uint_as_float(s16[1]));
+  const auto s32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(m), __float_as_uint(m), false, false);
+  return fmaxf(__uint_as_float(s32[0]), __uint_as_float(s32[1]));
+}
+
+struct P16State {
+  f32x4_t s[4][2];  // [kb][qb]
+  f32x4_t o[8][2];  // [db][qb]
+  f32x4_t negm[2];  // splat(-m_run[qb]): C operand of each tile's first QK^T MFMA
+  bf16x8_t pf[2][2];  // [ks2][qb]
+  bf16x8_t qf[2][4];  // [qb][ks]
+  float m_run[2], l_run[2];
+};
+
+__global__ void __launch_bounds__(512) attn16_kernel(AttnArgs a) {
+  __shared__ __attribute__((aligned(16))) char smem_raw[2 * kRing * kTileBytes];  // K ring, V ring
+  char QIE_LDS* smem = (char QIE_LDS*)smem_raw;
+
+  const int qbf = a.split ? a.qblocks - 1 : a.qblocks;
+  const int nfull = qbf * a.H * a.B;
+  int qblk, bh, chunk = -1;
+  if ((int)blockIdx.x < nfull) {
+    const int wgid = xcd_remap(blockIdx.x, nfull);
+    qblk = wgid % qbf;
+    bh = wgid / qbf;
+  } else {
+    const int j = blockIdx.x - nfull;
+    bh = j / a.split;
+    chunk = j - bh * a.split;
+    qblk = a.qblocks - 1;
+  }
+  const int h = bh % a.H, b = bh / a.H;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int grp = wave >> 2;
+  const int g = lane >> 4;
+  const int c = lane & 15;
+  const int64_t plane = (int64_t)a.s_pad * kDh;
+  const bf16_t* Qp = a.qkv + ((int64_t)(0 * a.B + b) * a.H + h) * plane;
+  const bf16_t* Kp = a.qkv + ((int64_t)(1 * a.B + b) * a.H + h) * plane;
+  const bf16_t* Vp = a.qkv + ((int64_t)(2 * a.B + b) * a.H + h) * plane;
+  const int kv_len = a.kv_len.v[b];
+  const int ntot = (kv_len + kKB - 1) / kKB;
+  const int t0 = chunk < 0 ? 0 : chunk * ntot / a.split;
+  const int ntiles = chunk < 0 ? ntot : (chunk + 1) * ntot / a.split;
+
+  P16State st;
+  const int q_wave = qblk * kQB + wave * 32;  // first query row of this wave
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    const bf16_t* qr = Qp + (int64_t)(q_wave + qb * 16 + c) * kDh + 8 * g;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) st.qf[qb][ks] = *(const bf16x8_t*)(qr + 32 * ks);
+  }
+
+  // ---- LDS-DMA: wave w fills rows 4(w + 8p) .. +3 of a tile (p = 0, 1) for K and for V
+  const auto kr = attn_rsrc(Kp, a.s_pad * kDh * 2);
+  const auto vr = attn_rsrc(Vp, a.s_pad * kDh * 2);
+  uint32_t ko[2], vo[2];
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const int row = (wave + 8 * p) * 4 + (lane >> 4), cc = lane & 15;
+    ko[p] = row * 256 + ((cc ^ (row & 15)) << 4);
+    vo[p] = row * 256 + ((cc ^ ((row & 3) << 2) ^ (((row >> 2) & 1) << 1)) << 4);
+  }
+  auto dmaK = [&](int t) {
+    char QIE_LDS* base = smem + (t % kRing) * kTileBytes;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) attn_dma_lean(kr, base + (wave + 8 * p) * 1024, ko[p], t * kTileBytes);
+  };
+  auto dmaV = [&](int t) {
+    char QIE_LDS* base = smem + (kRing + t % kRing) * kTileBytes;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) attn_dma_lean(vr, base + (wave + 8 * p) * 1024, vo[p], t * kTileBytes);
+  };
+
+  // per-lane LDS offsets: K row c of a 16-key block; V transposed-read lane (q, p) = (c >> 2, c & 3)
+  const int k_lane = c * 256;
+  const int tq = c >> 2, tp = c & 3;
+  const int v_sw = (tq << 1) ^ (g & 1);  // the V swizzle of rows 4g + tq, in units of 2 chunks
+  const int v_lane = (4 * g + tq) * 256 + ((tp >> 1) << 4) + 8 * (tp & 1);
+
+  // fragment f of an M-phase: f < 16 -> K (kb = f >> 2, ks = f & 3) of tile tk;
+  // f >= 16 -> V^T (ks2 = (f-16) >> 3, db = (f-16) & 7) of tile tv
+  auto opA = [&](int f, int tk, int tv) -> bf16x8_t {
+    if (f < 16) {
+      const int kb = f >> 2, ks = f & 3;
+      const char QIE_LDS* p = smem + (tk % kRing) * kTileBytes + kb * 16 * 256 + k_lane;
+      return *(const bf16x8_t QIE_LDS*)(p + (((4 * ks + g) ^ c) << 4));
+    }
+    const int j = f - 16, ks2 = j >> 3, db = j & 7;
+    const char QIE_LDS* p = smem + (kRing + tv % kRing) * kTileBytes + ks2 * 32 * 256 + v_lane +
+                            ((db ^ v_sw) << 5);
+    const s16x4_t v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((s16x4_t QIE_LDS*)p);
+    const s16x4_t v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((s16x4_t QIE_LDS*)(p + 16 * 256));
+    return __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7));
+  };
+  auto mfma_f = [&](int f, const bf16x8_t& A) {
+    if (f < 16) {
+      const int kb = f >> 2, ks = f & 3;
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) {
+        if (ks == 0) mma16_c(st.s[kb][qb], A, st.qf[qb][0], st.negm[qb]);
+        else mma16(st.s[kb][qb], A, st.qf[qb][ks]);
+      }
+    } else {
+      const int j = f - 16, ks2 = j >> 3, db = j & 7;
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) mma16(st.o[db][qb], A, st.pf[ks2][qb]);
+    }
+  };
+  auto mphase = [&](auto f0_t, auto f1_t, int tk, int tv) {
+    constexpr int f0 = decltype(f0_t)::value, f1 = decltype(f1_t)::value;
+    constexpr int PF = QIE_ATTN16_PF;
+    bf16x8_t A[8];
+    __builtin_amdgcn_s_setprio(QIE_ATTN_MPRIO);
+#pragma unroll
+    for (int f = f0; f < f0 + PF && f < f1; ++f) A[f & 7] = opA(f, tk, tv);
+#pragma unroll
+    for (int f = f0; f < f1; ++f) {
+      if (f + PF < f1) A[(f + PF) & 7] = opA(f + PF, tk, tv);
+      mfma_f(f, A[f & 7]);
+    }
+    __builtin_amdgcn_s_setprio(QIE_ATTN_VPRIO);
+  };
+  auto vphase = [&](int t) {
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) rfence(st.s[kb][qb]);
+#pragma unroll
+    for (int db = 0; db < 8; ++db)
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) rfence(st.o[db][qb]);
+    int pieces = 0;
+    if (t + 2 < ntiles) { dmaK(t + 2); pieces += 2; }
+    if (t + 1 < ntiles) { dmaV(t + 1); pieces += 2; }
+    const int kv0 = t * kKB;
+    if (kv0 + kKB > kv_len) {
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int kv = kv0 + kb * 16 + 4 * g + r;
+          if (kv >= kv_len) {
+            st.s[kb][0][r] = -INFINITY;
+            st.s[kb][1][r] = -INFINITY;
+          }
+        }
+    }
+    float mx[2];
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+      float m0 = fmaxf(st.s[0][qb][0], st.s[0][qb][1]), m1 = fmaxf(st.s[0][qb][2], st.s[0][qb][3]);
+#pragma unroll
+      for (int kb = 1; kb < 4; ++kb) {
+        m0 = fmaxf(m0, fmaxf(st.s[kb][qb][0], st.s[kb][qb][1]));
+        m1 = fmaxf(m1, fmaxf(st.s[kb][qb][2], st.s[kb][qb][3]));
+      }
+      mx[qb] = max_over_groups(fmaxf(m0, m1));
+    }
+    // S holds s*c - m_run (log2 units); tile t0 always rescales (it sets m_run)
+    if (__any(t == t0 || mx[0] > kRescaleThr || mx[1] > kRescaleThr)) {
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) {
+        const float d = t == t0 ? mx[qb] : fmaxf(mx[qb], 0.f);
+        const float alpha = __builtin_amdgcn_exp2f(-d);
+        st.m_run[qb] += d;
+        st.l_run[qb] *= alpha;
+#pragma unroll
+        for (int db = 0; db < 8; ++db) st.o[db][qb] *= alpha;
+#pragma unroll
+        for (int kb = 0; kb < 4; ++kb) st.s[kb][qb] -= d;
+        const float nm = -st.m_run[qb];
+        st.negm[qb] = f32x4_t{nm, nm, nm, nm};
+      }
+    }
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+      float ps0 = 0.f, ps1 = 0.f;
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb) {
+        const float p0 = __builtin_amdgcn_exp2f(st.s[kb][qb][0]);
+        const float p1 = __builtin_amdgcn_exp2f(st.s[kb][qb][1]);
+        const float p2 = __builtin_amdgcn_exp2f(st.s[kb][qb][2]);
+        const float p3 = __builtin_amdgcn_exp2f(st.s[kb][qb][3]);
+        ps0 += p0 + p2;
+        ps1 += p1 + p3;
+        const int e = (kb & 1) * 4;
+        st.pf[kb >> 1][qb][e] = (__bf16)p0;
+        st.pf[kb >> 1][qb][e + 1] = (__bf16)p1;
+        st.pf[kb >> 1][qb][e + 2] = (__bf16)p2;
+        st.pf[kb >> 1][qb][e + 3] = (__bf16)p3;
+      }
+      st.l_run[qb] += ps0 + ps1;
+    }
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) rfence(st.pf[k][qb]);
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+      rfence(st.l_run[qb]);
+      rfence(st.m_run[qb]);
+      rfence(st.negm[qb]);
+    }
+#pragma unroll
+    for (int db = 0; db < 8; ++db)
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) rfence(st.o[db][qb]);
+    if (pieces == 4) asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
+    else if (pieces == 2) asm volatile("s_waitcnt vmcnt(2)\n\ts_barrier" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+  };
+  using F0 = std::integral_constant<int, 0>;
+  using F16 = std::integral_constant<int, 16>;
+  using F32 = std::integral_constant<int, 32>;
+
+  float* po_base = nullptr;
+  float* pml = nullptr;
+  if (chunk >= 0) {
+    po_base = a.ws + ((int64_t)bh * a.split + chunk) * kQB * kDh;
+    pml = a.ws + (int64_t)a.B * a.H * a.split * kQB * kDh + ((int64_t)bh * a.split + chunk) * kQB * 2;
+  }
+  if (t0 >= ntiles) {  // empty key range (fewer tiles than ranges): neutral partial
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+      const int q_loc = wave * 32 + qb * 16 + c;
+#pragma unroll
+      for (int db = 0; db < 8; ++db)
+        *(f32x4_t*)(po_base + (int64_t)q_loc * kDh + 16 * db + 4 * g) = f32x4_t{0, 0, 0, 0};
+      if (g == 0) *(f32x2_t*)(pml + q_loc * 2) = f32x2_t{-INFINITY, 0.f};
+    }
+    return;
+  }
+  // ---- prologue: K(t0), K(t0+1), V(t0) resident; group 1 waits one phase
+  dmaK(t0);
+  if (t0 + 1 < ntiles) dmaK(t0 + 1);
+  dmaV(t0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_waitcnt(0);
+  asm volatile("s_barrier" ::: "memory");
+  if (grp == 1) asm volatile("s_barrier" ::: "memory");
+#pragma unroll
+  for (int db = 0; db < 8; ++db)
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) st.o[db][qb] = f32x4_t{};
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    st.m_run[qb] = 0.f;  // finite (it is the MFMA's C); tile t0 sets it
+    st.l_run[qb] = 0.f;
+    st.negm[qb] = f32x4_t{};
+  }
+
+  auto mend = [&]() { asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory"); };
+  mphase(F0{}, F16{}, t0, t0);  // S(t0)
+  mend();
+  vphase(t0);
+  for (int t = t0 + 1; t < ntiles; ++t) {
+    mphase(F0{}, F32{}, t, t - 1);  // S(t), O += V(t-1) P(t-1)
+    mend();
+    vphase(t);
+  }
+  mphase(F16{}, F32{}, t0, ntiles - 1);  // O += V(T-1) P(T-1)
+  if (grp == 0) asm volatile("s_barrier" ::: "memory");
+  // MFMA D -> VALU read hazard before the epilogue reads O (asm MFMAs are not padded by hipcc)
+#pragma unroll
+  for (int db = 0; db < 8; db += 2)
+    asm volatile("s_nop 7" : "+v"(st.o[db][0]), "+v"(st.o[db][1]), "+v"(st.o[db + 1][0]), "+v"(st.o[db + 1][1]));
+  asm volatile("s_nop 15" ::: "memory");
+  float l_tot[2];
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    float l = st.l_run[qb];
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    l_tot[qb] = l;
+  }
+  if (chunk >= 0) {  // fp32 partial: unnormalised O, row max, row sum
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+      const int q_loc = wave * 32 + qb * 16 + c;
+#pragma unroll
+      for (int db = 0; db < 8; ++db)
+        *(f32x4_t*)(po_base + (int64_t)q_loc * kDh + 16 * db + 4 * g) = st.o[db][qb];
+      if (g == 0) *(f32x2_t*)(pml + q_loc * 2) = f32x2_t{st.m_run[qb], l_tot[qb]};
+    }
+    return;
+  }
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    const int s = q_wave + qb * 16 + c;
+    bf16_t* dst = nullptr;
+    if (s < a.s_img) {
+      dst = a.out_img + ((int64_t)b * a.s_img + s) * (a.H * kDh) + h * kDh;
+    } else if (s < a.s_img + a.txt_rows) {
+      dst = a.out_txt + ((int64_t)b * a.txt_rows + (s - a.s_img)) * (a.H * kDh) + h * kDh;
+    }
+    const float inv = 1.0f / l_tot[qb];
+    // lane (g, c) holds d = 16db + 4g + 0..3; one permlane16 swap per dword of the pair (db, db+1)
+    // gives an even-g lane d = 16db + 4g .. +7 and an odd-g lane d = 16(db+1) + 4(g-1) .. +7
+#pragma unroll
+    for (int db = 0; db < 8; db += 2) {
+      const f32x4_t& x0 = st.o[db][qb];
+      const f32x4_t& x1 = st.o[db + 1][qb];
+      const unsigned w0x = pack2(x0[0] * inv, x0[1] * inv), w0y = pack2(x0[2] * inv, x0[3] * inv);
+      const unsigned w1x = pack2(x1[0] * inv, x1[1] * inv), w1y = pack2(x1[2] * inv, x1[3] * inv);
+      const auto sx = __builtin_amdgcn_permlane16_swap(w0x, w1x, false, false);
+      const auto sy = __builtin_amdgcn_permlane16_swap(w0y, w1y, false, false);
+      const int d0 = (g & 1) ? 16 * (db + 1) + 4 * (g - 1) : 16 * db + 4 * g;
+      if (dst) *(u32x4_t*)(dst + d0) = u32x4_t{sx[0], sy[0], sx[1], sy[1]};
+    }
+  }
+}
+
 // Merges the `split` partials of the last query block: O = sum_c w_c O_c / sum_c w_c l_c with
 // w_c = exp2((m_c - max_c m_c) * c). One wave per (b, h, row), two d values per lane.
 __global__ void __launch_bounds__(256) attn_combine_kernel(AttnArgs a) {
@@ -574,7 +922,8 @@ int launch_attn(AttnArgs& a, bool pre, void* workspace, int64_t workspace_bytes,
   const int64_t need = workspace ? split_bytes(a.B, a.H, a.qblocks) : 0;
   if (pre) a.c = 1.0f;  // logits already in log2 units (combine weights too)
   if (need == 0) {      // no workspace, or a single query block: nothing to split
-    if (pre) attn_pp_kernel<true><<<a.qblocks * a.H * a.B, 512, 0, s>>>(a);
+    if (pre && QIE_ATTN16) attn16_kernel<<<a.qblocks * a.H * a.B, 512, 0, s>>>(a);
+    else if (pre) attn_pp_kernel<true><<<a.qblocks * a.H * a.B, 512, 0, s>>>(a);
     else attn_pp_kernel<false><<<a.qblocks * a.H * a.B, 512, 0, s>>>(a);
     return qie_last_error();
   }
@@ -582,7 +931,8 @@ int launch_attn(AttnArgs& a, bool pre, void* workspace, int64_t workspace_bytes,
   a.split = QIE_ATTN_SPLIT;
   a.ws = (float*)workspace;
   const int grid = ((a.qblocks - 1) + a.split) * a.H * a.B;
-  if (pre) attn_pp_kernel<true><<<grid, 512, 0, s>>>(a);
+  if (pre && QIE_ATTN16) attn16_kernel<<<grid, 512, 0, s>>>(a);
+  else if (pre) attn_pp_kernel<true><<<grid, 512, 0, s>>>(a);
   else attn_pp_kernel<false><<<grid, 512, 0, s>>>(a);
   attn_combine_kernel<<<(a.B * a.H * kQB + 3) / 4, 256, 0, s>>>(a);
   return qie_last_error();
