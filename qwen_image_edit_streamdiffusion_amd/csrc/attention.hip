@@ -63,7 +63,10 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 // V live in 3-slot LDS rings filled by buffer_load...lds two tiles ahead. Waits: vmcnt(0) at
 // the end of an M-phase (this wave's pieces from its previous V-phase), vmcnt(pieces) at the
 // end of a V-phase; one barrier per phase.
-constexpr int kRing = 3;
+#ifndef QIE_ATTN_EARLY  // bit 0: 4-slot rings, DMA one tile further ahead, no vmcnt at the M-end;
+#define QIE_ATTN_EARLY 1  // bit 1: the next M-phase's first reads before the V-end barrier;
+#endif                    // bit 2: keep the M-end vmcnt(0)
+constexpr int kRing = (QIE_ATTN_EARLY & 1) ? 4 : 3;
 #ifndef QIE_ATTN_MPRIO  // issue priority of a wave in its MFMA phase
 #define QIE_ATTN_MPRIO 2
 #endif
@@ -276,15 +279,25 @@ __global__ void __launch_bounds__(512) attn_pp_kernel(AttnArgs a) {
     }
   };
   // M-phase over MFMAs [i0, i1): operands prefetched PF MFMAs ahead
-  auto mphase = [&](auto i0_t, auto i1_t, int tk, int tv) {
+  constexpr int PF = 5;  // operand prefetch distance in MFMAs (3: -0.7 %, 7: -0.3 %)
+  bf16x8_t A[8];
+  // EARLY: the first PF operands of an M-phase are read at the end of the preceding V-phase,
+  // before its barrier (their tiles landed two V-phases ago, see vphase), so the MFMAs start
+  // right behind the barrier instead of behind one LDS round trip
+  auto mpre = [&](int i0, int i1, int tk, int tv) {
+#pragma unroll
+    for (int i = 0; i < 32; ++i)
+      if (i >= i0 && i < i0 + PF && i < i1) A[i & 7] = opA(i, tk, tv);
+  };
+  auto mphase = [&](auto i0_t, auto i1_t, int tk, int tv, bool pre_read) {
     constexpr int i0 = decltype(i0_t)::value, i1 = decltype(i1_t)::value;
-    constexpr int PF = 5;  // operand prefetch distance in MFMAs (3: -0.7 %, 7: -0.3 %)
-    bf16x8_t A[8];
     // the MFMA wave outranks its SIMD partner (in its softmax phase) for issue: otherwise the
     // older wave group wins arbitration and starves the younger group's MFMA phase
     if (QIE_ATTN_STATIC < 0) __builtin_amdgcn_s_setprio(QIE_ATTN_MPRIO);
+    if (!pre_read) {
 #pragma unroll
-    for (int i = i0; i < i0 + PF && i < i1; ++i) A[i & 7] = opA(i, tk, tv);
+      for (int i = i0; i < i0 + PF && i < i1; ++i) A[i & 7] = opA(i, tk, tv);
+    }
 #pragma unroll
     for (int i = i0; i < i1; ++i) {
       if (i + PF < i1) A[(i + PF) & 7] = opA(i + PF, tk, tv);
@@ -303,8 +316,9 @@ __global__ void __launch_bounds__(512) attn_pp_kernel(AttnArgs a) {
     for (int db = 0; db < 4; ++db) rfence(st.o[db]);
     int pieces = 0;
     if (!(QIE_ATTN_ABL & 1)) {
-      if (t + 2 < ntiles) { dmaK(t + 2); pieces += 2; }
-      if (t + 1 < ntiles) { dmaV(t + 1); pieces += 2; }
+      constexpr int ahead = (QIE_ATTN_EARLY & 1) ? 1 : 0;  // EARLY: K(t+3), V(t+2)
+      if (t + 2 + ahead < ntiles) { dmaK(t + 2 + ahead); pieces += 2; }
+      if (t + 1 + ahead < ntiles) { dmaV(t + 1 + ahead); pieces += 2; }
     }
     const int kv0 = t * kKB;
     if (kv0 + kKB > kv_len) {
@@ -400,6 +414,13 @@ __global__ void __launch_bounds__(512) attn_pp_kernel(AttnArgs a) {
     if constexpr (PRE && QIE_ATTN_ONES) rfence(st.lsum);
 #pragma unroll
     for (int db = 0; db < 4; ++db) rfence(st.o[db]);
+    // EARLY: the next M-phase reads K(t+1) and V(t) (whole M-phase) or V(t) (the tail); their
+    // pieces were issued in V-phase t-2 and every wave's V-phase t-1 ended with vmcnt(pieces of
+    // t-1), i.e. with them landed, before the barrier that precedes this V-phase
+    if (QIE_ATTN_EARLY & 2) {
+      if (t + 1 < ntiles) mpre(0, 32, t + 1, t);
+      else mpre(16, 32, t0, t);
+    }
     if (pieces == 4) asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
     else if (pieces == 2) asm volatile("s_waitcnt vmcnt(2)\n\ts_barrier" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
@@ -418,10 +439,15 @@ __global__ void __launch_bounds__(512) attn_pp_kernel(AttnArgs a) {
     if (hf == 0) *(f32x2_t*)(pml + (((int64_t)bh * a.split + chunk) * kQB + q_loc) * 2) = f32x2_t{-INFINITY, 0.f};
     return;
   }
-  // ---- prologue: K(t0), K(t0+1), V(t0) resident; group 1 waits one phase
+  // ---- prologue: K(t0), K(t0+1), V(t0) resident (EARLY: + K(t0+2), V(t0+1)); group 1 waits
+  // one phase
   dmaK(t0);
   if (t0 + 1 < ntiles) dmaK(t0 + 1);
   dmaV(t0);
+  if (QIE_ATTN_EARLY & 1) {
+    if (t0 + 2 < ntiles) dmaK(t0 + 2);
+    if (t0 + 1 < ntiles) dmaV(t0 + 1);
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the asm DMA pieces
   __builtin_amdgcn_s_waitcnt(0);                     // Q fragments (hipcc-tracked)
   asm volatile("s_barrier" ::: "memory");
@@ -436,13 +462,17 @@ __global__ void __launch_bounds__(512) attn_pp_kernel(AttnArgs a) {
   if constexpr (PRE) st.negm = f32x16_t{};
   if constexpr (PRE && QIE_ATTN_ONES) st.lsum = f32x16_t{};
 
-  auto mend = [&](int) { asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory"); };
-  mphase(I0{}, I16{}, t0, t0);  // S(t0)
+  // EARLY: no vmcnt at the M-end (the V-end wait covers every tile two phases before its use)
+  auto mend = [&](int) {
+    if ((QIE_ATTN_EARLY & 5) == 1) asm volatile("s_barrier" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+  };
+  mphase(I0{}, I16{}, t0, t0, false);  // S(t0)
   mend(t0);
   vphase(t0);
   for (int t = t0 + 1; t < ntiles; ++t) {
     STAMP(t0);
-    mphase(I0{}, IMEND{}, t, t - 1);  // S(t), O += V(t-1) P(t-1)
+    mphase(I0{}, IMEND{}, t, t - 1, QIE_ATTN_EARLY & 2);  // S(t), O += V(t-1) P(t-1)
     STAMP(t1);
     mend(t);
     STAMP(t2);
@@ -457,7 +487,7 @@ __global__ void __launch_bounds__(512) attn_pp_kernel(AttnArgs a) {
   if (lane == 0)
     for (int i = 0; i < 4; ++i) atomicAdd(&g_stamp[grp][i], acc_st[i]);
 #endif
-  mphase(I16{}, IMEND{}, t0, ntiles - 1);  // O += V(T-1) P(T-1)
+  mphase(I16{}, IMEND{}, t0, ntiles - 1, QIE_ATTN_EARLY & 2);  // O += V(T-1) P(T-1)
   if (grp == 0) asm volatile("s_barrier" ::: "memory");
   // MFMA D -> VALU read hazard before the epilogue reads O (asm MFMAs are not padded by hipcc)
   asm volatile("s_nop 15\n\ts_nop 7" : "+v"(st.o[0]), "+v"(st.o[1]), "+v"(st.o[2]), "+v"(st.o[3]));

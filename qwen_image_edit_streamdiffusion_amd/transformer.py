@@ -21,6 +21,7 @@ HBM layout per forward (B rows, S_img image tokens, S_txt text tokens):
 from __future__ import annotations
 
 import contextlib
+import os
 from collections import OrderedDict
 from dataclasses import dataclass
 from typing import Dict, Iterator, List, Optional, Sequence, Tuple
@@ -540,7 +541,9 @@ class QwenImageTransformer2DModel(nn.Module):
         if not self.overlap_text_stream:
             return None
         if self._side is None:
-            self._side = torch.cuda.Stream(device=self.device)
+            # QIE_SIDE_PRIORITY (A/B): HIP stream priority of the text stream (lower = higher)
+            self._side = torch.cuda.Stream(device=self.device,
+                                           priority=int(os.environ.get("QIE_SIDE_PRIORITY", "0")))
         return self._side
 
     def _block(self, blk: _Block, ws: _Workspace, B, S_img, S_txt, kv_len, icos, isin, tcos, tsin, eps,
