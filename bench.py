@@ -139,9 +139,10 @@ def main():
                     help="A/B: image QKV GEMM and QK RMSNorm+RoPE as two launches")
     ap.add_argument("--no-log2q", action="store_true",
                     help="A/B: plain q and the softmax scale inside the attention (not log2-unit q)")
-    ap.add_argument("--text-splits", type=int, default=1,
+    ap.add_argument("--text-splits", default="1",
                     help="A/B: K ranges of the text-stream linears (1 = unsplit, the default; 0 = the "
-                         "latency-oriented split rule ops.splitk_splits)")
+                         "latency-oriented split rule ops.splitk_splits), or per linear as "
+                         "'down=0,up=2' (qkv / out / up / down; unnamed ones unsplit)")
     ap.add_argument("--no-text-overlap", action="store_true",
                     help="A/B: run the text stream on the caller's stream, not on a second HIP stream")
     ap.add_argument("--no-mod-cache", action="store_true",
@@ -178,7 +179,10 @@ def main():
     model.log2q_attention = not args.no_log2q
     model.batched_modulation = not args.no_batched_mod
     model.cache_modulation = not args.no_mod_cache
-    model.text_splits = args.text_splits or None
+    if "=" in args.text_splits:
+        model.text_splits = {k: int(v) for k, v in (kv.split("=") for kv in args.text_splits.split(","))}
+    else:
+        model.text_splits = int(args.text_splits) or None
     decode = args.vae in ("both", "decode")
     encode = args.vae == "both"
     vae = QwenImageVAEDecoder(device=dev).random_init_(seed=1) if decode else None

@@ -610,7 +610,7 @@ class QwenImageTransformer2DModel(nn.Module):
             inp = h
         qs = ops.LOG2Q_SCALE if self.log2q_attention else 1.0
         # one launch: GEMM + per-head RMSNorm + RoPE (the text stream too when its linears run unsplit)
-        if self.fuse_qk_norm_rope and (s == "img" or self.text_splits == 1):
+        if self.fuse_qk_norm_rope and (s == "img" or self._txt_splits("qkv", 3 * D, D) == 1):
             if self.int8:
                 wq8, sw = blk.q8[f"qkv_{s}"]
                 ops.linear_qkv_norm_rope_i8(qD, sc, wq8, sw, getattr(blk, f"b_qkv_{s}"), ws.qkv, rpb, seq_off,
@@ -655,7 +655,7 @@ class QwenImageTransformer2DModel(nn.Module):
         if isinstance(inp, tuple):
             (xq, sx), (wq, sw) = inp, blk.q8[f"{name}_{s}"]
             if s == "txt":
-                sp = self.text_splits or ops.splitk_splits(wq.shape[0], wq.shape[1], int8=True)
+                sp = self._txt_splits(name, wq.shape[0], wq.shape[1], int8=True)
                 return ops.linear_splitk_i8(xq, sx, wq, sw, b, kind, out, ws.splitk, sp, gate, rpb, seq_off)
             if kind == ops.EPI_QKV:
                 return ops.linear_qkv_i8(xq, sx, wq, sw, b, out, rpb, seq_off)
@@ -664,13 +664,21 @@ class QwenImageTransformer2DModel(nn.Module):
             return ops.linear_i8(xq, sx, wq, sw, b, out, act=ops.ACT_GELU if kind == ops.EPI_GELU else ops.ACT_NONE)
         w = getattr(blk, f"w_{name}_{s}")
         if s == "txt":
-            sp = self.text_splits or ops.splitk_splits(w.shape[0], w.shape[1])
+            sp = self._txt_splits(name, w.shape[0], w.shape[1])
             return ops.linear_splitk(inp, w, b, kind, out, ws.splitk, sp, gate, rpb, seq_off)
         if kind == ops.EPI_QKV:
             return ops.linear_qkv(inp, w, b, out, rpb, seq_off)
         if kind == ops.EPI_GATED_RESIDUAL:
             return ops.linear_gated_residual(inp, w, b, gate, rpb, out)
         return ops.linear(inp, w, b, out=out, act=ops.ACT_GELU if kind == ops.EPI_GELU else ops.ACT_NONE)
+
+    def _txt_splits(self, name: str, N: int, K: int, int8: bool = False) -> int:
+        """K ranges of text-stream linear ``name`` (qkv / out / up / down): ``text_splits`` is one
+        count for all, or a {name: count} dict (missing names: 1); 0 or None = ops.splitk_splits."""
+        ts = self.text_splits
+        if isinstance(ts, dict):
+            ts = ts.get(name, 1)
+        return ts or ops.splitk_splits(N, K, int8=int8)
 
     @contextlib.contextmanager
     def _probe(self, name: Optional[str]):
