@@ -95,6 +95,30 @@ def test_full_width_block_vs_oracle(dev):
     assert e <= 2e-2, e
 
 
+def test_text_split_configs_vs_oracle(dev):
+    """Text-stream linears split over K per linear (``text_splits`` dict, bench --text-splits):
+    fp32 partials + reduce change only the summation order, so every configuration stays within
+    the full-width bound of the oracle and close to the unsplit forward (rel-L2 <= 1e-2); the
+    fused text QKV + norm + RoPE launch is used only when the text QKV is unsplit."""
+    cfg = R.DiTConfig(num_layers=1)
+    params = R.random_params(cfg, seed=3)
+    m = make_model(cfg, params, dev)
+    shapes = [(1, 16, 16), (1, 16, 16)]
+    hs, enc = _inputs(2, shapes, 64, cfg.joint_attention_dim, seed=4)
+    enc[1, 40:] = 0
+    lens = [64, 40]
+    t = R.model_timestep(torch.tensor([1000.0, 20.0]))
+    ref = R.transformer_forward(params, cfg, hs, enc, t, shapes, lens)
+    outs = {}
+    for name, ts in (("unsplit", 1), ("down+out", {"down": 0, "out": 0}), ("qkv", {"qkv": 0}), ("all", None)):
+        m.text_splits = ts
+        outs[name] = m(hs.to(dev), enc.to(dev), None, t.to(dev), [shapes] * 2, lens, return_dict=False)[0].clone()
+        assert rel(outs[name], ref) <= 2e-2, (name, rel(outs[name], ref))
+    m.text_splits = 1
+    for name in ("down+out", "qkv", "all"):
+        assert rel(outs[name], outs["unsplit"]) <= 1e-2, name
+
+
 def _pipe(m):
     from qwen_image_edit_streamdiffusion_amd import QwenImageEditPlusPipeline
     return QwenImageEditPlusPipeline(m)
