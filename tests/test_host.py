@@ -296,3 +296,23 @@ def test_prompt_cache_keys_on_reference_image():
     assert not c.is_valid("p", a)
     c.reference_key = c.image_key(a)
     assert c.is_valid("p", Image.new("RGB", (8, 8), "red")) and not c.is_valid("p", b)
+
+
+def test_text_split_rule_and_per_linear_config():
+    """Text-stream split-K counts (bench --text-splits): one count for all linears, a per-linear
+    dict (names missing from it unsplit), or 0 / None = ops.splitk_splits, which depends on
+    (N, K) only (so batched CFG == sequential) and always divides the K tiles."""
+    m = QwenImageTransformer2DModel.__new__(QwenImageTransformer2DModel)
+    D, F = 3072, 12288
+    shapes = {"qkv": (3 * D, D), "out": (D, D), "up": (F, D), "down": (D, F)}
+    for name, (N, K) in shapes.items():
+        s = ops.splitk_splits(N, K)
+        assert s >= 1 and (K * 2 // 128) % s == 0
+        assert 2 * -(-N // 256) * s <= 256 or s == 1
+        m.text_splits = 1
+        assert m._txt_splits(name, N, K) == 1
+        m.text_splits = None
+        assert m._txt_splits(name, N, K) == s
+        m.text_splits = {"down": 0, "up": 3}
+        assert m._txt_splits(name, N, K) == {"down": s, "up": 3}.get(name, 1)
+    assert [ops.splitk_splits(*shapes[n]) for n in ("qkv", "out", "up", "down")] == [3, 4, 2, 8]
