@@ -154,6 +154,14 @@ def main():
         M = B * S_IMG
         res.append(bench_i8("i8_up", M, F, D, act=1))
         res.append(bench_i8("i8_down", M, D, F))
+    if "i8x" in want:  # int8 per-tile overhead: K = 3072 (12 tiles per CU) vs K = 12288 (3 per CU)
+        M = B * S_IMG
+        res.append(bench_i8("i8_up_plain", M, F, D, act=0))
+        res.append(bench_i8("i8_up_gelu", M, F, D, act=1))
+        res.append(bench_i8("i8_down_plain", M, D, F, act=0))
+        res.append(bench_i8("i8_out_plain", M, D, D, act=0))
+        res.append(bench_gemm("mlp_up_plain", M, F, D, "plain"))
+        res.append(bench_gemm("out_plain", M, D, D, "plain"))
     if not want or "qkv" in want:
         res += bench_qkv_variants()
     if not want or "misc" in want:
