@@ -39,7 +39,15 @@ import os
 import sys
 import time
 
-import torch
+# HIP hardware queues per process, set before HIP initialises (first torch.cuda call). RCCL's own
+# streams (process group, N > 1) otherwise share HIP's default 4 queues with the model's two
+# streams, the text-stream overlap (transformer._side_stream) serialises behind the image stream
+# and every step costs ~9 % more: 290.8 vs 266.4 ms at N = 1 under --force-dist, 265.7 with 8
+# queues (tools/dist_ab.sh, profiles/round2_s5_dist_ab.txt).
+if int(os.environ.get("GPU_MAX_HW_QUEUES") or 0) < 8:  # raise an inherited 4, keep a larger value
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
+
+import torch  # noqa: E402
 import torch.distributed as dist
 
 ROOT = os.path.dirname(os.path.abspath(__file__))

@@ -20,6 +20,7 @@ HIP transformer and libqie kernels.
 from __future__ import annotations
 
 import os
+import warnings
 from dataclasses import dataclass
 from typing import Callable, List, Optional, Sequence
 
@@ -33,6 +34,10 @@ def init_distributed(backend: Optional[str] = None):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and torch.cuda.is_initialized() and int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 8:
+        warnings.warn("HIP initialised with fewer than 8 hardware queues: RCCL's streams will share "
+                      "them with the transformer's text-stream overlap, which then serialises (~9 % "
+                      "per step); export GPU_MAX_HW_QUEUES=8 before the first HIP call")
     use_cuda = torch.cuda.is_available() and backend != "gloo"
     device = torch.device("cuda", local) if use_cuda else torch.device("cpu")
     if use_cuda:
