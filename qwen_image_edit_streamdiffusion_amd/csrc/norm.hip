@@ -42,7 +42,13 @@ __device__ __forceinline__ u32x2_t quant8(const float f[8], float inv) {
 #ifndef QIE_LNMOD_PREFETCH
 #define QIE_LNMOD_PREFETCH 0  // measured slower: 42.0 vs 39.3 us (register pressure), kept as a build option
 #endif
-template <bool I8>
+#ifndef QIE_LNMOD_EXACT  // 1: chunk count per lane as a template argument where D = 512 * NC (no guards,
+#define QIE_LNMOD_EXACT 1  // x kept packed: 102 -> fewer VGPRs, more waves in flight); 0: generic only
+#endif
+// NC: 16-byte chunks per lane (EXACT: every lane has exactly NC, D = 512 * NC); the bf16 path keeps
+// x packed (4 VGPRs per chunk) and unpacks it for each pass; the int8 path also keeps the modulated
+// values for the quantisation pass. Same arithmetic and order in every instantiation.
+template <bool I8, int NC, bool EXACT>
 __global__ void __launch_bounds__(256)
     ln_mod_kernel(const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __restrict__ shift,
                   const bf16_t* __restrict__ scale, int64_t mod_bstride, int rpb, void* QIE_LNMOD_YR y, int64_t ldy,
@@ -52,15 +58,29 @@ __global__ void __launch_bounds__(256)
   const int lane = threadIdx.x & 63;
   const int nch = D >> 3;
   const bf16_t* xr = x + (int64_t)row * ldx;
-  float v[kMaxC][8];
+  u32x4_t raw[EXACT ? NC : 1];   // EXACT: x packed, unpacked again by each pass
+  float xf[EXACT ? 1 : NC][8];   // generic: x unpacked once (fewer VGPRs for the guarded form)
+  auto get = [&](int i, float f[8]) {
+    if constexpr (EXACT) unpack8(raw[i], f);
+    else
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] = xf[i][j];
+  };
+  float v[I8 ? NC : 1][8];
   float sum = 0.f;
 #pragma unroll
-  for (int i = 0; i < kMaxC; ++i) {
+  for (int i = 0; i < NC; ++i) {
     const int c = lane + 64 * i;
-    if (c < nch) {
-      unpack8(*(const u32x4_t*)(xr + c * 8), v[i]);
+    if (EXACT || c < nch) {
+      const u32x4_t w = *(const u32x4_t*)(xr + c * 8);
+      float f[8];
+      unpack8(w, f);
+      if constexpr (EXACT) raw[i] = w;
+      else
 #pragma unroll
-      for (int j = 0; j < 8; ++j) sum += v[i][j];
+        for (int j = 0; j < 8; ++j) xf[i][j] = f[j];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sum += f[j];
     }
   }
   const int b = row / rpb;
@@ -69,31 +89,43 @@ __global__ void __launch_bounds__(256)
 #if QIE_LNMOD_PREFETCH
   // scale / shift issued with x, under the two reductions: in the store loop below hipcc may not
   // move chunk i+1's loads above chunk i's store (y may alias them), one round trip per chunk
-  u32x4_t scv[kMaxC], shv[kMaxC];
+  u32x4_t scv[NC], shv[NC];
 #pragma unroll
-  for (int i = 0; i < kMaxC; ++i) {
+  for (int i = 0; i < NC; ++i) {
     const int c = min(lane + 64 * i, nch - 1);
     scv[i] = *(const u32x4_t*)(sc + c * 8);
     shv[i] = *(const u32x4_t*)(sh + c * 8);
   }
 #endif
   const float mean = wave_sum(sum) / (float)D;
+  // the passes re-unpack x from the packed registers: without these fences hipcc keeps all 8 * NC
+  // unpacked floats live across the reductions (CSE of the three unpacks)
+  if constexpr (EXACT)
+#pragma unroll
+    for (int i = 0; i < NC; ++i) asm volatile("" : "+v"(raw[i]));
   float sq = 0.f;
 #pragma unroll
-  for (int i = 0; i < kMaxC; ++i)
-    if (lane + 64 * i < nch)
+  for (int i = 0; i < NC; ++i)
+    if (EXACT || lane + 64 * i < nch) {
+      float f[8];
+      get(i, f);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const float d = v[i][j] - mean;
+        const float d = f[j] - mean;
         sq += d * d;
       }
+    }
   const float rstd = rsqrtf(wave_sum(sq) / (float)D + eps);
+  if constexpr (EXACT)
+#pragma unroll
+    for (int i = 0; i < NC; ++i) asm volatile("" : "+v"(raw[i]));
   float amax = 0.f;
 #pragma unroll
-  for (int i = 0; i < kMaxC; ++i) {
+  for (int i = 0; i < NC; ++i) {
     const int c = lane + 64 * i;
-    if (c < nch) {
-      float s8[8], h8[8];
+    if (EXACT || c < nch) {
+      float f[8], s8[8], h8[8];
+      get(i, f);
 #if QIE_LNMOD_PREFETCH
       unpack8(scv[i], s8);
       unpack8(shv[i], h8);
@@ -103,12 +135,17 @@ __global__ void __launch_bounds__(256)
 #endif
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const float n = rbf((v[i][j] - mean) * rstd);
+        const float n = rbf((f[j] - mean) * rstd);
         const float t = rbf(n * rbf(1.0f + s8[j]));
-        v[i][j] = rbf(t + h8[j]);
-        amax = fmaxf(amax, fabsf(v[i][j]));
+        f[j] = rbf(t + h8[j]);
+        amax = fmaxf(amax, fabsf(f[j]));
       }
-      if constexpr (!I8) *(u32x4_t*)((bf16_t*)y + (int64_t)row * ldy + c * 8) = pack8(v[i]);
+      if constexpr (I8) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[i][j] = f[j];
+      } else {
+        *(u32x4_t*)((bf16_t*)y + (int64_t)row * ldy + c * 8) = pack8(f);
+      }
     }
   }
   if constexpr (I8) {
@@ -116,12 +153,31 @@ __global__ void __launch_bounds__(256)
     const float inv = amax > 0.f ? 127.0f / amax : 0.f;
     int8_t* qr = (int8_t*)y + (int64_t)row * ldy;
 #pragma unroll
-    for (int i = 0; i < kMaxC; ++i) {
+    for (int i = 0; i < NC; ++i) {
       const int c = lane + 64 * i;
-      if (c < nch) *(u32x2_t*)(qr + c * 8) = quant8(v[i], inv);
+      if (EXACT || c < nch) *(u32x2_t*)(qr + c * 8) = quant8(v[i], inv);
     }
     if (lane == 0) qscale[row] = amax > 0.f ? amax / 127.0f : 1.0f;
   }
+}
+
+// one launch of ln_mod_kernel: the exact-chunk instantiation for D = 3072 / 3584 / 4096
+template <bool I8>
+void launch_ln_mod(const void* x, int64_t ldx, const void* shift, const void* scale, int64_t mod_bstride,
+                   int rpb, void* y, int64_t ldy, float* qscale, int rows, int D, float eps, hipStream_t s) {
+  const dim3 grid((rows + 3) / 4), block(256);
+  const auto* xp = (const bf16_t*)x;
+  const auto* shp = (const bf16_t*)shift;
+  const auto* scp = (const bf16_t*)scale;
+  if (QIE_LNMOD_EXACT && D == 512 * 6)
+    ln_mod_kernel<I8, 6, true><<<grid, block, 0, s>>>(xp, ldx, shp, scp, mod_bstride, rpb, y, ldy, qscale, rows, D, eps);
+  else if (QIE_LNMOD_EXACT && D == 512 * 7)
+    ln_mod_kernel<I8, 7, true><<<grid, block, 0, s>>>(xp, ldx, shp, scp, mod_bstride, rpb, y, ldy, qscale, rows, D, eps);
+  else if (QIE_LNMOD_EXACT && D == 512 * 8)
+    ln_mod_kernel<I8, 8, true><<<grid, block, 0, s>>>(xp, ldx, shp, scp, mod_bstride, rpb, y, ldy, qscale, rows, D, eps);
+  else
+    ln_mod_kernel<I8, kMaxC, false><<<grid, block, 0, s>>>(xp, ldx, shp, scp, mod_bstride, rpb, y, ldy, qscale, rows, D,
+                                                           eps);
 }
 
 __global__ void __launch_bounds__(256)
@@ -239,9 +295,8 @@ extern "C" int qie_layernorm_modulate_bf16(const void* x, int64_t ldx, const voi
   QIE_CHECK_ARG(x && shift && scale && y && rows > 0 && rows_per_batch > 0);
   QIE_CHECK_ARG(D % 8 == 0 && D <= 64 * 8 * kMaxC && ldx % 8 == 0 && ldy % 8 == 0);
   QIE_CHECK_ARG(mod_bstride % 8 == 0);
-  ln_mod_kernel<false><<<(rows + 3) / 4, 256, 0, (hipStream_t)stream>>>(
-      (const bf16_t*)x, ldx, (const bf16_t*)shift, (const bf16_t*)scale, mod_bstride, rows_per_batch,
-      y, ldy, nullptr, rows, D, eps);
+  launch_ln_mod<false>(x, ldx, shift, scale, mod_bstride, rows_per_batch, y, ldy, nullptr, rows, D, eps,
+                       (hipStream_t)stream);
   return qie_last_error();
 }
 
@@ -252,9 +307,8 @@ extern "C" int qie_layernorm_modulate_i8(const void* x, int64_t ldx, const void*
   QIE_CHECK_ARG(x && shift && scale && q && qscale && rows > 0 && rows_per_batch > 0);
   QIE_CHECK_ARG(D % 8 == 0 && D <= 64 * 8 * kMaxC && ldx % 8 == 0 && ldq % 8 == 0);
   QIE_CHECK_ARG(mod_bstride % 8 == 0);
-  ln_mod_kernel<true><<<(rows + 3) / 4, 256, 0, (hipStream_t)stream>>>(
-      (const bf16_t*)x, ldx, (const bf16_t*)shift, (const bf16_t*)scale, mod_bstride, rows_per_batch,
-      q, ldq, qscale, rows, D, eps);
+  launch_ln_mod<true>(x, ldx, shift, scale, mod_bstride, rows_per_batch, q, ldq, qscale, rows, D, eps,
+                      (hipStream_t)stream);
   return qie_last_error();
 }
 
