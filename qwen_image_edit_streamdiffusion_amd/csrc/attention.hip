@@ -79,6 +79,9 @@ constexpr int kRing = (QIE_ATTN_EARLY & 1) ? 4 : 3;
 #ifndef QIE_ATTN_ONES  // 1: row sums by 4 MFMAs against a ones operand in the MFMA phase (log2q path)
 #define QIE_ATTN_ONES 0
 #endif
+#ifndef QIE_ATTN_PKSUM  // 1: the log2-q softmax's row sums as packed f32x2 adds
+#define QIE_ATTN_PKSUM 0  // measured 8 % slower (1.413 -> 1.530 ms): packed FP32 beside the partner wave's MFMAs
+#endif
 #ifndef QIE_ATTN_ABL  // diagnostic ablations (wrong results): 1 no K/V DMA in the loop, 2 no exp2
 #define QIE_ATTN_ABL 0
 #endif
@@ -344,8 +347,9 @@ __global__ void __launch_bounds__(512) attn_pp_kernel(AttnArgs a) {
     };
     float ps0 = 0.f, ps1 = 0.f;
     auto exp_tile = [&]() {  // P = exp2(S), row sums, bf16 P^T fragments
-      ps0 = 0.f;
-      ps1 = 0.f;
+      // the two interleaved row-sum chains as one f32x2 (v_pk_add_f32: 16 adds per tile, not 32;
+      // same per-chain order, so the same bits)
+      f32x2_t ps = {0.f, 0.f};
 #pragma unroll
       for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
@@ -353,12 +357,20 @@ __global__ void __launch_bounds__(512) attn_pp_kernel(AttnArgs a) {
           const float p0 = __builtin_amdgcn_exp2f(st.s[cb][r]);
           const float p1 = __builtin_amdgcn_exp2f(st.s[cb][r + 1]);
           if (!(PRE && QIE_ATTN_ONES)) {
-            ps0 += p0;
-            ps1 += p1;
+            if constexpr (QIE_ATTN_PKSUM) {
+              ps += f32x2_t{p0, p1};
+            } else {
+              ps0 += p0;
+              ps1 += p1;
+            }
           }
           st.pf[cb * 2 + (r >> 3)][r & 7] = (__bf16)p0;
           st.pf[cb * 2 + (r >> 3)][(r & 7) + 1] = (__bf16)p1;
         }
+      if constexpr (QIE_ATTN_PKSUM) {
+        ps0 = ps.x;
+        ps1 = ps.y;
+      }
     };
     if constexpr (PRE) {
       // S already holds s*c - m_run (log2 units); tile t0 always rescales (it sets m_run)
