@@ -286,6 +286,50 @@ __global__ void __launch_bounds__(256)
   if (lane == 0) scale[row] = amax > 0.f ? amax / 127.0f : 1.0f;
 }
 
+// Two waves per row (D = 1024 * NCW, the int8 path's GELU output at D = 12288): each wave holds
+// NCW chunks per lane (48 VGPRs of x at NCW = 12 instead of 96), the two wave maxima meet in LDS.
+// amax is a max, so the result is bit-identical to quant_rows_kernel. Rows past `rows` still reach
+// the barrier.
+#ifndef QIE_QUANT_2W
+#define QIE_QUANT_2W 1
+#endif
+template <int NCW>
+__global__ void __launch_bounds__(256)
+    quant_rows2_kernel(const bf16_t* __restrict__ x, int64_t ldx, int8_t* __restrict__ q, int64_t ldq,
+                       float* __restrict__ scale, int rows) {
+  __shared__ float wmax[4];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 2 + (wave >> 1), half = wave & 1;
+  const bool valid = row < rows;
+  const int c0 = half * 64 * NCW + lane;  // this lane's first chunk of the row
+  const bf16_t* xr = x + (int64_t)(valid ? row : 0) * ldx;
+  u32x4_t raw[NCW];
+  float amax = 0.f;
+  if (valid) {
+#pragma unroll
+    for (int i = 0; i < NCW; ++i) {
+      raw[i] = *(const u32x4_t*)(xr + (c0 + 64 * i) * 8);
+      float f[8];
+      unpack8(raw[i], f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf(f[j]));
+    }
+  }
+  amax = wave_max(amax);
+  if (lane == 0) wmax[wave] = amax;
+  __syncthreads();
+  if (!valid) return;
+  amax = fmaxf(wmax[wave & 2], wmax[(wave & 2) + 1]);
+  const float inv = amax > 0.f ? 127.0f / amax : 0.f;
+#pragma unroll
+  for (int i = 0; i < NCW; ++i) {
+    float f[8];
+    unpack8(raw[i], f);
+    *(u32x2_t*)(q + (int64_t)row * ldq + (c0 + 64 * i) * 8) = quant8(f, inv);
+  }
+  if (half == 0 && lane == 0) scale[row] = amax > 0.f ? amax / 127.0f : 1.0f;
+}
+
 }  // namespace
 
 extern "C" int qie_layernorm_modulate_bf16(const void* x, int64_t ldx, const void* shift,
@@ -342,7 +386,9 @@ extern "C" int qie_quantize_rows_i8(const void* x, int64_t ldx, void* q, int64_t
   QIE_CHECK_ARG(x && q && scale && rows > 0 && D % 8 == 0 && ldx % 8 == 0 && ldq % 8 == 0);
   hipStream_t s = (hipStream_t)stream;
   const int grid = (rows + 3) / 4;
-  if (D <= 64 * 8 * 8)
+  if (QIE_QUANT_2W && D == 1024 * 12)
+    quant_rows2_kernel<12><<<(rows + 1) / 2, 256, 0, s>>>((const bf16_t*)x, ldx, (int8_t*)q, ldq, scale, rows);
+  else if (D <= 64 * 8 * 8)
     quant_rows_kernel<8><<<grid, 256, 0, s>>>((const bf16_t*)x, ldx, (int8_t*)q, ldq, scale, rows, D);
   else if (D <= 64 * 8 * 24)
     quant_rows_kernel<24><<<grid, 256, 0, s>>>((const bf16_t*)x, ldx, (int8_t*)q, ldq, scale, rows, D);

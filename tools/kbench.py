@@ -162,6 +162,13 @@ def main():
         res.append(bench_i8("i8_out_plain", M, D, D, act=0))
         res.append(bench_gemm("mlp_up_plain", M, F, D, "plain"))
         res.append(bench_gemm("out_plain", M, D, D, "plain"))
+    if "i8q" in want:  # per-row int8 quantisation of the GELU output / attention output (int8 path)
+        for name, D_ in (("quant_mlp", F), ("quant_att", D)):
+            xx = rnd(B * S_IMG, D_)
+            qq = torch.empty(B * S_IMG, D_, dtype=torch.int8, device=dev)
+            ss = torch.empty(B * S_IMG, dtype=torch.float32, device=dev)
+            ms = timeit(lambda: ops.quantize_rows(xx, qq, ss))
+            res.append(f"{name} rows={B * S_IMG} D={D_}: {ms * 1e3:.1f} us  {3.0 * B * S_IMG * D_ / ms / 1e9:.2f} TB/s")
     if not want or "qkv" in want:
         res += bench_qkv_variants()
     if not want or "misc" in want:
