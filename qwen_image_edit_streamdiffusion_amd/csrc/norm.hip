@@ -66,7 +66,10 @@ __global__ void __launch_bounds__(256)
 #pragma unroll
       for (int j = 0; j < 8; ++j) f[j] = xf[i][j];
   };
-  float v[I8 ? NC : 1][8];
+  // int8: the modulated row for the quant pass -- packed (bf16-exact values) in the exact form,
+  // as floats in the generic one (fewer VGPRs for each)
+  u32x4_t vp[I8 && EXACT ? NC : 1];
+  float vf[I8 && !EXACT ? NC : 1][8];
   float sum = 0.f;
 #pragma unroll
   for (int i = 0; i < NC; ++i) {
@@ -140,9 +143,11 @@ __global__ void __launch_bounds__(256)
         f[j] = rbf(t + h8[j]);
         amax = fmaxf(amax, fabsf(f[j]));
       }
-      if constexpr (I8) {
+      if constexpr (I8 && EXACT) {
+        vp[i] = pack8(f);  // exact: every f[j] is already a bf16 value
+      } else if constexpr (I8) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[i][j] = f[j];
+        for (int j = 0; j < 8; ++j) vf[i][j] = f[j];
       } else {
         *(u32x4_t*)((bf16_t*)y + (int64_t)row * ldy + c * 8) = pack8(f);
       }
@@ -155,7 +160,15 @@ __global__ void __launch_bounds__(256)
 #pragma unroll
     for (int i = 0; i < NC; ++i) {
       const int c = lane + 64 * i;
-      if (EXACT || c < nch) *(u32x2_t*)(qr + c * 8) = quant8(v[i], inv);
+      if (EXACT || c < nch) {
+        if constexpr (EXACT) {
+          float g[8];
+          unpack8(vp[i], g);
+          *(u32x2_t*)(qr + c * 8) = quant8(g, inv);
+        } else {
+          *(u32x2_t*)(qr + c * 8) = quant8(vf[i], inv);
+        }
+      }
     }
     if (lane == 0) qscale[row] = amax > 0.f ? amax / 127.0f : 1.0f;
   }
