@@ -369,6 +369,7 @@ def main():
                        "parallelism": f"frame-shard x{world}" if world > 1 else "single"},
             "sec_per_image": sec_per_image,
             "host_io": host_io,
+            "hip_hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES") or 0),
             "mfma_util": flops_img * images / el / (peak * world),
             "tflops_per_gpu": flops_img * images / el / world / 1e12,
             "roofline": roof, "kernels": kernels, "cpu_baseline": cpu,
