@@ -16,14 +16,26 @@ completes is VAE-decoded to uint8 RGB (unpack + de-normalise + post_quant_conv
 both.  In steady state every step completes one image, so images/sec =
 completed frames / time.  Synthetic inputs (randn / randint with fixed seeds)
 are resident in HBM before the timed region.  The text encoder is not on this
-path: the prompt embedding comes from the prompt cache.
+path: the prompt embedding comes from the prompt cache (SURVEY.md §8 f2);
+--vl-per-frame puts it on the path (the reference's realtime call re-encodes
+the prompt with every frame, qwen_realtime.py:247-255).
+
+The same JSON line carries, under "secondary", the like-for-like workloads of
+the reference's published numbers, each timed the same way right after the
+headline (same process, same model): "stream2-cfg" (true CFG 4.0 as
+benchmark_lightning.py:28-29 / qwen_realtime.py:247-255 run it: B = 4 rows per
+frame), "stream2-int8" (configs[3]) and, on an even number of ranks > 1,
+"stream2-cfg-pairs" (configs[4]: cond / uncond on the two ranks of a pair,
+pairs x frame shard).
 
 Multi-GPU (torch.distributed.run, one process per GPU, RCCL): each rank runs
 its own stream engine on its own frames (frame shard, weak scaling); rank 0
 broadcasts the prompt embeddings once and gathers every finished image
-(uint8 RGB, 3 MiB / frame; the 512 KiB latent with --no-decode) inside the
-timed loop.  value = frames of all ranks / max
-rank time.
+(uint8 RGB, 3 MiB / frame; the 512 KiB latent with --vae none) inside the
+timed loop.  value = frames of all ranks / max rank time.  --cfg-parallel
+(workload stream2-cfg): ranks 2k / 2k+1 carry the cond / uncond rows of the
+same frames and exchange the noise predictions with one all_gather per frame
+(parallel.CFGPairStreamDenoiser); the pairs shard the frames.
 
 Also emitted: roofline of the dominant kernel (HIP events around each launch
 on its stream inside the timed region), and a CPU baseline: the oracle's fp32
@@ -48,7 +60,7 @@ if int(os.environ.get("GPU_MAX_HW_QUEUES") or 0) < 8:  # raise an inherited 4, k
     os.environ["GPU_MAX_HW_QUEUES"] = "8"
 
 import torch  # noqa: E402
-import torch.distributed as dist
+import torch.distributed as dist  # noqa: E402
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
@@ -58,6 +70,16 @@ PEAK_BF16 = 2.5e15     # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, spec)
 PEAK_I8 = 5.0e15       # i8 MFMA: 2x bf16 per clock
 S_NOISE = S_COND = 4096
 S_TXT = 216
+D_MODEL, F_MLP, N_LAYERS_FULL = 3072, 12288, 60
+
+WORKLOADS = {
+    "stream2": "lightning-2step stream-batch depth=2, cond-only, 1024x1024 (configs[2])",
+    "stream2-int8": "int8 W8A8 linears, lightning-2step stream-batch depth=2, 1024x1024 (configs[3])",
+    "stream2-cfg": "lightning-2step stream-batch depth=2 + true-CFG 4.0 (B=4), 1024x1024",
+    "stream2-cfg-pairs": "lightning-2step stream-batch depth=2 + true-CFG 4.0, cond / uncond on the two ranks "
+                         "of a pair (one all_gather per frame), pairs x frame shard, 1024x1024 (configs[4])",
+    "cfg4": "4-step true-CFG 4.0 batched cond/uncond, 1024x1024 (configs[1])",
+}
 
 
 def log(*a):
@@ -65,50 +87,48 @@ def log(*a):
         print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(decode: bool = True, encode: bool = True):
-    """Oracle (torch fp32 on the host cores) on a bounded sample of the SAME
-    workload: one B=2 stream-batch forward with 1 of the 60 blocks (prologue +
-    block + head) at full size, scaled x60 -> sec/image (1 forward/image)."""
+def _cpu_model() -> str:
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(sample_layers: int = 3):
+    """The oracle (torch fp32 on the host cores) on BASELINE configs[0], the reference's own
+    CPU-runnable case: 256x256 output (256 noise tokens) + the 1024^2-area condition image
+    Edit-Plus always encodes (4096 tokens) + 216 text tokens, 2 steps, cond-only, random-init
+    weights of the real width. Bounded sample: ``sample_layers`` of the 60 blocks (the blocks are
+    identical in cost), scaled x60/sample_layers -> sec/image."""
     from oracle import dit_ref as R
     n = min(16, len(os.sched_getaffinity(0)))
     torch.set_num_threads(n)
-    cfg = R.DiTConfig(num_layers=1)
+    cfg = R.DiTConfig(num_layers=sample_layers)
     params = R.random_params(cfg, seed=0)
     g = torch.Generator().manual_seed(0)
-    hs = torch.randn(2, S_NOISE + S_COND, 64, generator=g).to(BF16)
-    enc = torch.randn(2, S_TXT, cfg.joint_attention_dim, generator=g).to(BF16)
-    t = R.model_timestep(torch.tensor([1000.0, 20.0]))
-    shapes = [(1, 64, 64), (1, 64, 64)]
+    noise = torch.randn(1, 256, 64, generator=g).to(BF16)
+    cond = torch.randn(1, S_COND, 64, generator=g).to(BF16)
+    pe = torch.randn(1, S_TXT, cfg.joint_attention_dim, generator=g).to(BF16)
+    shapes = [(1, 16, 16), (1, 64, 64)]
     t0 = time.time()
-    R.transformer_forward(params, cfg, hs, enc, t, shapes, [S_TXT, S_TXT], emulate_bf16=False)
+    R.denoise(params, cfg, noise, cond, pe, shapes, 2, emulate_bf16=False)
     dt = time.time() - t0
-    sec_per_image = dt * 60
-    sample = (f"oracle fp32 torch-CPU: one B=2 stream-batch forward with 1 of 60 DiT blocks at full 1024^2 size "
-              f"({dt:.1f} s), scaled x60")
-    if decode:  # VAE decode of the real architecture at 32x32 latents (256^2), scaled by FLOPs to 128x128
-        from oracle import vae_ref as V
-        vc = V.VAEConfig()
-        vp = V.random_params(vc, 1)
-        packed = torch.randn(1, 256, 64, generator=g).to(BF16)
-        t0 = time.time()
-        V.decode(vp, packed, 32, 32, vc, emulate_bf16=False)
-        dv = (time.time() - t0) * V.decode_flops(vc, 128, 128) / V.decode_flops(vc, 32, 32)
-        sec_per_image += dv
-        sample += f" + VAE decode (256^2 sample, FLOP-scaled to 1024^2: {dv:.1f} s)"
-    if encode:  # VAE encode of a 256^2 frame, scaled by FLOPs to 1024^2
-        from oracle import vae_ref as V
-        vc = V.VAEConfig()
-        ep = V.random_encoder_params(vc, 2)
-        rgb = torch.randint(0, 256, (1, 256, 256, 3), generator=g, dtype=torch.uint8)
-        t0 = time.time()
-        V.encode(ep, rgb, vc, emulate_bf16=False)
-        from qwen_image_edit_streamdiffusion_amd.vae import QwenImageVAEEncoder, VAEConfig
-        ef = QwenImageVAEEncoder(VAEConfig(), "cpu")
-        de = (time.time() - t0) * ef.flops(1024, 1024) / ef.flops(256, 256)
-        sec_per_image += de
-        sample += f" + VAE encode (256^2 sample, FLOP-scaled: {de:.1f} s)"
-    return {"value": 1.0 / sec_per_image, "unit": "images/sec", "cores": n, "kind": "port",
-            "sample": sample + f" = {sec_per_image:.0f} s/image", "sec_per_image": sec_per_image}
+    scale = N_LAYERS_FULL / sample_layers
+    sec_per_image = dt * scale
+    flops = 2 * R.flops_per_forward(256 + S_COND, S_TXT, R.DiTConfig(), layers=sample_layers)
+    rate = flops / dt  # FLOP/s the host cores reach on this path
+    head = 2 * R.flops_per_forward(S_NOISE + S_COND, S_TXT, R.DiTConfig())
+    return {"value": 1.0 / sec_per_image, "unit": "images/sec (256x256 output, configs[0])", "cores": n,
+            "cpu": _cpu_model(), "kind": "port",
+            "sample": (f"oracle fp32 torch-CPU, configs[0]: 256x256 output + 1024^2 condition image, 2 steps, "
+                       f"cond-only, B=1, S=4568, DiT denoise loop only (no VAE / prompt encoder); "
+                       f"{sample_layers} of 60 blocks timed ({dt:.1f} s), scaled x{scale:.0f} = "
+                       f"{sec_per_image:.0f} s/image"),
+            "sec_per_image": sec_per_image, "tflops": rate / 1e12,
+            "headline_workload_estimate_sec_per_image": head / rate}
 
 
 @contextlib.contextmanager
@@ -126,6 +146,11 @@ def _stdout_to_stderr():
         os.close(saved)
 
 
+def attention_flops(rows: int, layers: int = 1) -> float:
+    S = S_NOISE + S_COND + S_TXT
+    return 4.0 * rows * S * S * D_MODEL * layers
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -139,6 +164,15 @@ def main():
                          "the finished one (both, the default), decode only (condition frames arrive as "
                          "latents), or none (DiT denoise alone)")
     ap.add_argument("--no-probe", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="skip the secondary workloads (stream2-cfg, stream2-int8, stream2-cfg-pairs) that the "
+                         "default stream2 run times after the headline")
+    ap.add_argument("--cfg-parallel", action="store_true",
+                    help="workload stream2-cfg with the cond / uncond rows on the two ranks of a pair "
+                         "(configs[4]); needs an even number of ranks, or one rank with --force-dist")
+    ap.add_argument("--vl-per-frame", action="store_true",
+                    help="re-encode the prompt with every frame through the HIP Qwen2.5-VL (7B widths, random "
+                         "weights, vision cache off) inside the timed step, as qwen_realtime.py:247-255 does")
     ap.add_argument("--host-io", action="store_true",
                     help="PCIe-inclusive rate (never the headline): condition frames start in pinned host "
                          "memory and are copied to HBM inside the timed step, every finished image is "
@@ -168,6 +202,9 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist_on = world > 1 or args.force_dist
+    if args.cfg_parallel and (args.workload != "stream2-cfg" or not dist_on or (world > 1 and world % 2)):
+        raise SystemExit("--cfg-parallel needs --workload stream2-cfg and an even number of ranks "
+                         "(or one rank with --force-dist)")
     if dist_on:
         # RCCL prints a version banner on stdout when the communicator is created; stdout must
         # carry only the one JSON line, so fd 1 points at stderr until the first barrier is done
@@ -177,11 +214,10 @@ def main():
 
     from qwen_image_edit_streamdiffusion_amd import (QwenImageTransformer2DModel, StreamBatchDenoiser,
                                                      QwenImageEditPlusPipeline)
+    from qwen_image_edit_streamdiffusion_amd import parallel
     from qwen_image_edit_streamdiffusion_amd.vae import QwenImageVAEDecoder, QwenImageVAEEncoder
     t_build = time.time()
     model = QwenImageTransformer2DModel(num_layers=args.layers, device=dev).random_init_(seed=0)
-    if args.workload == "stream2-int8":
-        model.quantize_int8()
     model.overlap_text_stream = not args.no_text_overlap
     model.fuse_qk_norm_rope = not args.no_qk_fusion
     model.log2q_attention = not args.no_log2q
@@ -199,180 +235,265 @@ def main():
     log(f"[bench] model built in {time.time() - t_build:.1f}s, "
         f"{torch.cuda.memory_allocated() / 1e9:.1f} GB")
 
+    # pair groups (CFG parallel) and the delivery group are created by every rank, in the same
+    # order, before any of them is used
+    pairs_possible = dist_on and (world == 1 or world % 2 == 0)
+    pair_group = pair_role = pair_size = None
+    deliver_group = None
+    if pairs_possible and (args.cfg_parallel or (args.workload == "stream2" and not args.no_secondary and world > 1)):
+        pair_group, pair_role, pair_size = parallel.make_pair_groups(world)
+        heads = list(range(0, world, pair_size))
+        deliver_group = dist.new_group(ranks=heads)
+
     # ---- synthetic inputs, resident in HBM before timing
     g = torch.Generator(device=dev).manual_seed(44)
     pe = torch.randn(1, S_TXT, 3584, generator=g, device=dev, dtype=BF16)
+    ne = torch.randn(1, 211, 3584, generator=g, device=dev, dtype=BF16)  # shorter negative prompt
     if dist_on:
         dist.broadcast(pe, 0)  # prompt-embed cache filled once, from rank 0
-    gr = torch.Generator(device=dev).manual_seed(1000 + rank)
+        dist.broadcast(ne, 0)
     nf = 8
-    conds = [torch.randn(1, S_COND, 64, generator=gr, device=dev, dtype=BF16) for _ in range(nf)]
-    noises = [torch.randn(1, S_NOISE, 64, generator=gr, device=dev, dtype=BF16) for _ in range(nf)]
-    if encode:  # condition frames as camera images: uint8 RGB 1024x1024, resident in HBM
-        frames = [torch.randint(0, 256, (1, 1024, 1024, 3), generator=gr, device=dev, dtype=torch.uint8)
-                  for _ in range(nf)]
+
+    def make_inputs(seed):
+        gr = torch.Generator(device=dev).manual_seed(seed)
+        conds = [torch.randn(1, S_COND, 64, generator=gr, device=dev, dtype=BF16) for _ in range(nf)]
+        noises = [torch.randn(1, S_NOISE, 64, generator=gr, device=dev, dtype=BF16) for _ in range(nf)]
+        frames = None
+        if encode:  # condition frames as camera images: uint8 RGB 1024x1024, resident in HBM
+            frames = [torch.randint(0, 256, (1, 1024, 1024, 3), generator=gr, device=dev, dtype=torch.uint8)
+                      for _ in range(nf)]
+        return conds, noises, frames
+
     host_io = args.host_io and encode and decode
     if args.host_io and not host_io:
         raise SystemExit("--host-io needs --vae both (RGB frames in and out)")
-    if host_io:  # the frames live in pinned host memory; the step uploads them (stream-ordered)
-        frames_host = [f.cpu().pin_memory() for f in frames]
-        out_host = torch.empty(1, 1024, 1024, 3, dtype=torch.uint8).pin_memory()
+    out_host = torch.empty(1, 1024, 1024, 3, dtype=torch.uint8).pin_memory() if host_io else None
 
-    def frame(i):
-        if host_io:
-            return frames_host[i % nf].to(dev, non_blocking=True)
-        return frames[i % nf]
+    vl = None
+    if args.vl_per_frame:  # Qwen2.5-VL-7B on the HIP path, random weights; synthetic processor outputs
+        from qwen_image_edit_streamdiffusion_amd.text_encoder import (QwenVLEncoder, TextEncoderConfig,
+                                                                      random_state_dict, text_state_dict_shapes)
+        from qwen_image_edit_streamdiffusion_amd.vision import VisionConfig, vision_state_dict_shapes
+        tc, vc = TextEncoderConfig(), VisionConfig()
+        sd = {"model.language_model." + k: v
+              for k, v in random_state_dict(text_state_dict_shapes(tc), dev, 0).items()}
+        sd.update({"model.visual." + k: v for k, v in random_state_dict(vision_state_dict_shapes(vc), dev, 1).items()})
+        enc_vl = QwenVLEncoder(tc, vc, dev, vision_cache_size=0).load_state_dict(sd)
+        del sd
+        # Edit-Plus prompt: 64 template tokens (dropped), "Picture 1:" + a 392^2 condition image
+        # (28x28 patches -> 196 image tokens) + the instruction: 280 tokens -> 216 embeddings
+        ids = torch.randint(0, 150000, (64 + S_TXT,), generator=torch.Generator().manual_seed(5))
+        ids[70:70 + 196] = enc_vl.image_token_id
+        gv = torch.Generator(device=dev).manual_seed(6)
+        pvs = [torch.randn(28 * 28, vc.patch_dim, generator=gv, device=dev) for _ in range(nf)]
+        vl = (enc_vl, ids, pvs, [(1, 28, 28)])
 
-    probe_keys = ("attention", "mlp_up")
-    if args.workload.startswith("stream2"):
-        cfg_on = args.workload == "stream2-cfg"
-        eng = StreamBatchDenoiser(model, num_steps=2, true_cfg_scale=4.0 if cfg_on else 1.0,
-                                  latent_hw=(64, 64), cond_hw=(64, 64))
-        if cfg_on:  # true CFG 4.0 with a shorter negative prompt: cond + uncond rows, B = 4
-            ne = torch.randn(1, 211, 3584, generator=g, device=dev, dtype=BF16)
-            eng.set_conditions(pe, None, ne)
+    def run(workload: str, steps: int, warmup: int, probe: bool):
+        """Time `steps` steps of one workload on this rank's frames; returns its result dict
+        (rank 0) with the whole-job value."""
+        int8 = workload == "stream2-int8"
+        cfg_pairs = workload == "stream2-cfg-pairs"
+        cfg_on = workload in ("stream2-cfg", "stream2-cfg-pairs")
+        if int8 and not model.int8:
+            model.quantize_int8()
+        model.int8 = int8
+        shard = rank // pair_size if cfg_pairs else rank  # both ranks of a pair push the same frames
+        conds, noises, frames = make_inputs(1000 + shard)
+        frames_host = [f.cpu().pin_memory() for f in frames] if host_io else None
+
+        def frame(i):
+            if host_io:
+                return frames_host[i % nf].to(dev, non_blocking=True)
+            return frames[i % nf]
+
+        head = True  # this rank decodes and delivers finished frames
+        if workload == "cfg4":  # 4-step true-CFG 4.0, batched cond/uncond (B=2), one image per step
+            pipe = QwenImageEditPlusPipeline(model)
+            pipe.vae, pipe.vae_encoder = vae, vae_enc
+            rows_local = rows_total = 2
+            fwd_per_step = 4
+
+            def step(i):
+                src = dict(image=frame(i)) if encode else dict(image_latents=conds[i % nf])
+                return pipe(prompt_embeds=pe, negative_prompt_embeds=ne, latents=noises[i % nf], true_cfg_scale=4.0,
+                            num_inference_steps=4, output_type="uint8" if decode else "latent", **src).images
         else:
-            eng.set_conditions(pe)
-        rows = 4 if cfg_on else 2
-        fwd_per_step = 1
+            if cfg_pairs:
+                eng = parallel.CFGPairStreamDenoiser(model, num_steps=2, true_cfg_scale=4.0, latent_hw=(64, 64),
+                                                     cond_hw=(64, 64), role=pair_role, group=pair_group,
+                                                     group_size=pair_size)
+                head = pair_role == 0
+            else:
+                eng = StreamBatchDenoiser(model, num_steps=2, true_cfg_scale=4.0 if cfg_on else 1.0,
+                                          latent_hw=(64, 64), cond_hw=(64, 64))
+            eng.set_conditions(pe, None, ne if cfg_on else None)
+            rows_local = eng.rows
+            rows_total = 4 if cfg_on else 2
+            fwd_per_step = 1
 
-        def step(i):
-            cond = vae_enc.encode(frame(i)) if encode else conds[i % nf]
-            return eng.push(noises[i % nf], cond)
-    else:  # cfg4: 4-step true-CFG 4.0, batched cond/uncond (B=2), one image per step
-        pipe = QwenImageEditPlusPipeline(model)
-        ne = torch.randn(1, 211, 3584, generator=g, device=dev, dtype=BF16)
-        rows = 2
-        fwd_per_step = 4
+            def step(i):
+                cond = vae_enc.encode(frame(i)) if encode else conds[i % nf]
+                if vl is not None:  # this frame's own prompt embedding: vision tower + language model
+                    enc_vl, ids, pvs, grid = vl
+                    h = enc_vl(ids, pvs[i % nf], grid)[64:]
+                    return eng.push(noises[i % nf], cond, prompt_embeds=h, negative_prompt_embeds=None)
+                return eng.push(noises[i % nf], cond)
 
-        pipe.vae, pipe.vae_encoder = vae, vae_enc
+        n_heads = world // pair_size if cfg_pairs else world
+        grp = deliver_group if cfg_pairs else None
+        gather_buf = None
+        if dist_on and rank == 0:
+            gather_buf = [torch.empty(1, 1024, 1024, 3, dtype=torch.uint8, device=dev) if decode else
+                          torch.empty(1, S_NOISE, 64, dtype=BF16, device=dev) for _ in range(n_heads)]
 
-        def step(i):
-            src = dict(image=frame(i)) if encode else dict(image_latents=conds[i % nf])
-            return pipe(prompt_embeds=pe, negative_prompt_embeds=ne, latents=noises[i % nf], true_cfg_scale=4.0,
-                        num_inference_steps=4, output_type="uint8" if decode else "latent", **src).images
+        def deliver(res):
+            if not head:  # the uncond rank of a pair holds the same latents; its partner delivers them
+                return
+            out = res[1] if isinstance(res, tuple) else res
+            if decode and out.dtype != torch.uint8:  # stream engine: decode the frame that completed
+                out = vae.decode(out, 128, 128)
+            if host_io:  # D2H of the finished image, ordered on the compute stream
+                out_host.copy_(out.reshape(out_host.shape), non_blocking=True)
+            if dist_on:
+                dist.gather(out, gather_buf if rank == 0 else None, dst=0, group=grp)
 
-    gather_buf = None
-    if dist_on and rank == 0:
-        gather_buf = [torch.empty(1, 1024, 1024, 3, dtype=torch.uint8, device=dev) if decode else
-                      torch.empty(1, S_NOISE, 64, dtype=BF16, device=dev) for _ in range(world)]
-
-    def deliver(res):
-        out = res[1] if isinstance(res, tuple) else res
-        if decode and out.dtype != torch.uint8:  # stream engine: decode the frame that completed
-            out = vae.decode(out, 128, 128)
-        if host_io:  # D2H of the finished image, ordered on the compute stream
-            out_host.copy_(out.reshape(out_host.shape), non_blocking=True)
+        for i in range(warmup):
+            r = step(i)
+            if r is not None:
+                deliver(r)
+        if workload != "cfg4" and warmup < 2:
+            r = step(warmup)  # fill the 2-deep pipeline
+            warmup += 1
+            if r is not None:
+                deliver(r)
+        torch.cuda.synchronize()
+        model.probe = {k: [] for k in ("attention", "mlp_up")} if probe else None
         if dist_on:
-            dist.gather(out, gather_buf if rank == 0 else None, dst=0)
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.time()
+        done = 0
+        for i in range(steps):
+            r = step(warmup + i)
+            if r is not None:
+                done += 1 if head else 0
+                deliver(r)
+        torch.cuda.synchronize()
+        if dist_on:
+            dist.barrier()
+        el = time.time() - t0
+        if dist_on:
+            tt = torch.tensor([el], device=dev, dtype=torch.float64)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            el = tt.item()
+            dn = torch.tensor([done], device=dev, dtype=torch.float64)
+            dist.all_reduce(dn, op=dist.ReduceOp.SUM)
+            done = int(dn.item())
+        model_probe, model.probe = model.probe, None
 
-    for i in range(args.warmup):
-        r = step(i)
-        if r is not None:
-            deliver(r)
-    if args.workload.startswith("stream2") and args.warmup < 2:
-        step(args.warmup)  # fill the 2-deep pipeline
-    torch.cuda.synchronize()
-    if not args.no_probe:
-        model.probe = {k: [] for k in probe_keys}
-    if dist_on:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.time()
-    done = 0
-    for i in range(args.steps):
-        r = step(args.warmup + i)
-        if r is not None:
-            done += 1
-            deliver(r)
-    torch.cuda.synchronize()
-    if dist_on:
-        dist.barrier()
-    el = time.time() - t0
-    if dist_on:
-        tt = torch.tensor([el], device=dev, dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        el = tt.item()
-        dn = torch.tensor([done], device=dev, dtype=torch.float64)
-        dist.all_reduce(dn, op=dist.ReduceOp.SUM)
-        done = int(dn.item())
-    model_probe, model.probe = model.probe, None
+        images = done
+        S = S_NOISE + S_COND + S_TXT
+        flops_fwd = model.flops_per_forward(S_NOISE + S_COND, S_TXT, B=rows_total)
+        attn_fwd = attention_flops(rows_total, args.layers)
+        vae_flops = (vae.flops(128, 128) if decode else 0.0) + (vae_enc.flops(1024, 1024) if encode else 0.0)
+        flops_img = flops_fwd * fwd_per_step + vae_flops
+        # time the MFMA roof allows per image: int8 runs the linears at the i8 rate, the attention
+        # and the VAE at the bf16 rate (blended roof)
+        lin_peak = PEAK_I8 if int8 else PEAK_BF16
+        roof_s_img = ((flops_fwd - attn_fwd) * fwd_per_step / lin_peak +
+                      (attn_fwd * fwd_per_step + vae_flops) / PEAK_BF16)
+        kernels = {}
+        if model_probe:
+            alg = {"attention": attention_flops(rows_local),
+                   "mlp_up": 2.0 * rows_local * (S_NOISE + S_COND) * F_MLP * D_MODEL}
+            for k, evs in model_probe.items():
+                if not evs:
+                    continue
+                ms = [a.elapsed_time(b) for a, b in evs]
+                avg = sum(ms) / len(ms)
+                kpeak = PEAK_BF16 if k == "attention" else lin_peak
+                kernels[k] = {"avg_ms": avg, "launches": len(ms), "total_ms": sum(ms),
+                              "tflops": alg[k] / (avg * 1e-3) / 1e12, "frac": alg[k] / (avg * 1e-3) / kpeak}
+        roof = None
+        if kernels:
+            dom = max(kernels, key=lambda k: kernels[k]["total_ms"])
+            kd = kernels[dom]
+            kpeak = PEAK_BF16 if dom == "attention" else lin_peak
+            # HBM bytes per launch of this kernel: NOT measured by this run (PMC counters need
+            # rocprofv3 passes of their own); the figure of the committed passes over this same
+            # command (tools/measure.sh -> profiles/pmc_traffic.json), for the headline workload only
+            traffic = None
+            tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+            if os.path.exists(tf) and workload == "stream2":
+                t = json.load(open(tf)).get("traffic_per_launch", {}).get(dom)
+                traffic = t and t.get("hbm_bytes_per_launch")
+            roof = {"bound": "mfma", "kernel": dom, "achieved": kd["tflops"], "peak": kpeak / 1e12,
+                    "unit": "TFLOP/s", "frac": kd["frac"], "traffic": traffic,
+                    "traffic_source": "profiles/pmc_traffic.json (separate rocprofv3 --pmc passes)" if traffic else None,
+                    "flops_per_launch": (attention_flops(rows_local) if dom == "attention"
+                                         else 2.0 * rows_local * (S_NOISE + S_COND) * F_MLP * D_MODEL),
+                    "avg_launch_ms": kd["avg_ms"]}
+        par = "single"
+        if world > 1 or cfg_pairs:
+            par = (f"cfg-pair x{pair_size} x frame-shard x{n_heads}" if cfg_pairs else f"frame-shard x{world}")
+        return {
+            "value": images / el, "unit": "images/sec", "steps": steps, "warmup": warmup,
+            "ms_per_step": el / steps * 1e3, "sec_per_image": el * n_heads / max(images, 1),
+            "dtype": "int8" if int8 else "bf16",
+            "config": {"workload": WORKLOADS[workload] + (", prompt re-encoded per frame by Qwen2.5-VL-7B "
+                                                          "(random weights)" if vl is not None else ""),
+                       "model": "Qwen-Image-Edit-2509 DiT (60 blocks, D=3072)" +
+                                (" + AutoencoderKLQwenImage " + ("encoder/decoder" if encode else "decoder")
+                                 if decode else ""),
+                       "global_batch": rows_local * world, "seq_len": S, "layers": args.layers,
+                       "parallelism": par},
+            # fraction of the MFMA roof over the whole step: bf16 peak; int8: blended roof (linears
+            # at the i8 rate, attention + VAE at the bf16 rate)
+            "mfma_util": roof_s_img * images / el / world,
+            "tflops_per_gpu": flops_img * images / el / world / 1e12,
+            "roofline": roof, "kernels": kernels,
+        }
 
-    images = done
-    value = images / el
-    sec_per_image = el * world / max(images, 1)
-    S = S_NOISE + S_COND + S_TXT
-    flops_fwd = model.flops_per_forward(S_NOISE + S_COND, S_TXT, B=rows)
-    flops_img = (flops_fwd * fwd_per_step + (vae.flops(128, 128) if decode else 0.0) +
-                 (vae_enc.flops(1024, 1024) if encode else 0.0))
-    peak = PEAK_I8 if args.workload.endswith("int8") else PEAK_BF16
+    wl = "stream2-cfg-pairs" if args.cfg_parallel else args.workload
+    res = run(wl, args.steps, args.warmup, not args.no_probe)
 
-    kernels = {}
-    if model_probe:
-        D, F = 3072, 12288
-        alg = {"attention": 4.0 * rows * S * S * D,
-               "mlp_up": 2.0 * rows * (S_NOISE + S_COND) * F * D}
-        for k, evs in model_probe.items():
-            if not evs:
-                continue
-            ms = [a.elapsed_time(b) for a, b in evs]
-            avg = sum(ms) / len(ms)
-            kpeak = PEAK_BF16 if k == "attention" else peak
-            kernels[k] = {"avg_ms": avg, "launches": len(ms), "total_ms": sum(ms),
-                          "tflops": alg[k] / (avg * 1e-3) / 1e12, "frac": alg[k] / (avg * 1e-3) / kpeak}
-    roof = None
-    if kernels:
-        dom = max(kernels, key=lambda k: kernels[k]["total_ms"])
-        kd = kernels[dom]
-        kpeak = PEAK_BF16 if dom == "attention" else peak
-        # HBM bytes per launch of this kernel from the committed rocprofv3 FETCH_SIZE /
-        # WRITE_SIZE passes (tools/measure.sh + tools/summarize_profile.py), if present
-        traffic = None
-        tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-        if os.path.exists(tf) and args.workload == "stream2":
-            t = json.load(open(tf)).get("traffic_per_launch", {}).get(dom)
-            traffic = t and t.get("hbm_bytes_per_launch")
-        roof = {"bound": "mfma", "kernel": dom, "achieved": kd["tflops"], "peak": kpeak / 1e12,
-                "unit": "TFLOP/s", "frac": kd["frac"], "traffic": traffic,
-                "flops_per_launch": (4.0 * rows * S * S * 3072 if dom == "attention"
-                                     else 2.0 * rows * (S_NOISE + S_COND) * 12288 * 3072),
-                "avg_launch_ms": kd["avg_ms"]}
+    secondary = {}
+    if args.workload == "stream2" and not args.no_secondary and not args.vl_per_frame and not host_io:
+        names = ["stream2-cfg"]
+        if pair_group is not None and world > 1:
+            names.append("stream2-cfg-pairs")
+        names.append("stream2-int8")  # last: it quantises the model's linears
+        for name in names:
+            r = run(name, args.steps, min(args.warmup, 2), not args.no_probe)
+            secondary[name] = {k: r[k] for k in ("value", "unit", "ms_per_step", "sec_per_image", "dtype",
+                                                 "mfma_util", "tflops_per_gpu", "roofline", "config")}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
-            cpu = cpu_baseline(decode, encode)
+            cpu = cpu_baseline()
         except Exception as e:  # reported, never fatal to the GPU number
             cpu = {"error": repr(e)}
 
     if rank == 0:
-        workload = {"stream2": "lightning-2step stream-batch depth=2, cond-only, 1024x1024 (configs[2])",
-                    "stream2-int8": "int8 W8A8 linears, lightning-2step stream-batch depth=2, 1024x1024 "
-                                    "(configs[3])",
-                    "stream2-cfg": "lightning-2step stream-batch depth=2 + true-CFG 4.0 (B=4), 1024x1024",
-                    "cfg4": "4-step true-CFG 4.0 batched cond/uncond, 1024x1024 (configs[1])"}[args.workload]
         line = {
             "metric": "images/sec, 1024x1024 2-step Lightning edit (" +
+                      ("Qwen2.5-VL prompt encode + " if vl is not None else "") +
                       ("VAE encode + " if encode else "") + "DiT denoise" + (" + VAE decode" if decode else "") +
                       (", PCIe-inclusive: pinned host RGB in/out)" if host_io else ")"),
-            "value": value, "unit": "images/sec", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None,
-            "dtype": "int8" if args.workload.endswith("int8") else "bf16",
+            "value": res["value"], "unit": "images/sec", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": res["ms_per_step"], "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": res["dtype"],
             "data": "synthetic (randn latents/cond/prompt embeds; random-init weights of the real "
                     "60-block architecture)",
-            "config": {"workload": workload,
-                       "model": "Qwen-Image-Edit-2509 DiT (60 blocks, D=3072)" +
-                                (" + AutoencoderKLQwenImage " + ("encoder/decoder" if encode else "decoder")
-                                 if decode else ""),
-                       "global_batch": rows * world, "seq_len": S, "layers": args.layers,
-                       "parallelism": f"frame-shard x{world}" if world > 1 else "single"},
-            "sec_per_image": sec_per_image,
+            "config": res["config"],
+            "sec_per_image": res["sec_per_image"],
             "host_io": host_io,
             "hip_hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES") or 0),
-            "mfma_util": flops_img * images / el / (peak * world),
-            "tflops_per_gpu": flops_img * images / el / world / 1e12,
-            "roofline": roof, "kernels": kernels, "cpu_baseline": cpu,
+            "mfma_util": res["mfma_util"],
+            "tflops_per_gpu": res["tflops_per_gpu"],
+            "roofline": res["roofline"], "kernels": res["kernels"], "cpu_baseline": cpu,
+            "secondary": secondary or None,
         }
         print(json.dumps(line), flush=True)
     if dist_on:

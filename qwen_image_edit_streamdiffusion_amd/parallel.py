@@ -13,19 +13,19 @@
 
 Backend "nccl" is RCCL over xGMI on ROCm.  Messages are <= 1.5 MB against a
 ~190 ms forward, so they are latency-bound; no ring all-reduce, no TP/SP.
-The compute is injected (``forward``/``combine``/``step`` callables) so the
-exchange logic runs unchanged on CPU + gloo in tests; the defaults are the
-HIP transformer and libqie kernels.
+The engines take their arithmetic as an object (``stream.HipStreamCompute`` by
+default), so the exchange logic runs unchanged on CPU + gloo in tests.
 """
 from __future__ import annotations
 
 import os
 import warnings
-from dataclasses import dataclass
-from typing import Callable, List, Optional, Sequence
+from typing import Callable, List, Optional, Sequence, Tuple
 
 import torch
 import torch.distributed as dist
+
+from .stream import StreamBatchDenoiser
 
 
 def init_distributed(backend: Optional[str] = None):
@@ -84,80 +84,64 @@ def frame_owner(frame_idx: int, n_shards: int) -> int:
 
 def make_pair_groups(world: int):
     """All ranks create every pair group in the same order (torch requirement);
-    returns (my_pair_group, my_role) with role 0 = cond, 1 = uncond."""
-    if world % 2:
-        raise ValueError("CFG parallel needs an even number of ranks")
+    returns (my_pair_group, my_role, group_size) with role 0 = cond, 1 = uncond. World size 1 is a
+    pair of one (that rank computes both branches, group_size 1)."""
+    if world > 1 and world % 2:
+        raise ValueError("CFG parallel needs an even number of ranks (or a single one)")
     rank = dist.get_rank()
+    if world == 1:
+        return dist.new_group(ranks=[0]), 0, 1
     mine = None
     for k in range(world // 2):
         g = dist.new_group(ranks=[2 * k, 2 * k + 1])
         if rank // 2 == k:
             mine = g
-    return mine, rank % 2
+    return mine, rank % 2, 2
 
 
-@dataclass
-class CFGParallelDenoiser:
-    """Denoise one frame per pair; this rank computes one CFG branch.
+class CFGPairStreamDenoiser(StreamBatchDenoiser):
+    """The stream-batch engine with its two CFG branches on the two ranks of a pair.
 
-    forward(x_model_input, step_index) -> noise prediction [B, S_noise, C] of
-    THIS rank's branch (its own prompt/negative embeddings captured inside);
-    combine(cond, uncond, scale) -> guided prediction; step(x, v, i) -> next x.
-    """
+    Rank 2k (role 0) carries the cond rows of the ``depth`` in-flight frames, rank 2k + 1 (role 1)
+    the uncond rows of the SAME frames: both ranks push the same noise and condition latents.
+    Per pushed frame each rank runs one forward of ``depth`` rows, then ONE ``all_gather`` inside
+    the pair moves the noise predictions (depth x 512 KiB at 1024^2), and both ranks apply the
+    true-CFG combine and the per-row Euler step to identical inputs -- identical latents on both
+    ranks afterwards, nothing is sent back. A branch's rows see the shapes they have in the
+    batched-CFG engine (text padded to the longer prompt), and every kernel computes batch rows
+    independently, so the result equals StreamBatchDenoiser's batched CFG bit for bit.
 
-    forward: Callable[[torch.Tensor, int], torch.Tensor]
-    combine: Callable[[torch.Tensor, torch.Tensor, float], torch.Tensor]
-    step: Callable[[torch.Tensor, torch.Tensor, int], torch.Tensor]
-    scale: float
-    group: object = None
+    ``group`` of one rank (a pair of one: world size 1, or a left-over rank): that rank computes
+    both branches and the collective still runs, over the one-rank group.
+    ``exchange``: replaces the collective (single-process tests wire two engines together with
+    begin() / finish())."""
 
-    def denoise(self, x: torch.Tensor, num_steps: int) -> torch.Tensor:
-        for i in range(num_steps):
-            v_local = self.forward(x, i).contiguous()
-            parts = [torch.empty_like(v_local) for _ in range(2)]
-            dist.all_gather(parts, v_local, group=self.group)  # [cond, uncond] by pair order
-            v = self.combine(parts[0], parts[1], self.scale)
-            x = self.step(x, v, i)
-        return x
+    def __init__(self, transformer, num_steps: int = 2, true_cfg_scale: float = 4.0,
+                 latent_hw: Tuple[int, int] = (64, 64), cond_hw: Tuple[int, int] = (64, 64),
+                 scheduler=None, compute=None, role: int = 0, group=None, group_size: Optional[int] = None,
+                 exchange: Optional[Callable[[torch.Tensor], List[torch.Tensor]]] = None):
+        super().__init__(transformer, num_steps, true_cfg_scale, latent_hw, cond_hw, scheduler, compute)
+        if true_cfg_scale <= 1.0:
+            raise ValueError("CFG pairs need true_cfg_scale > 1 (cond-only runs have one branch)")
+        if group_size is None:
+            group_size = 2 if exchange is not None else dist.get_world_size(group)
+        if group_size not in (1, 2) or role not in (0, 1) or (group_size == 1 and role != 0):
+            raise ValueError("a CFG pair has one or two ranks, roles 0 (cond) and 1 (uncond)")
+        self.role, self.group, self.group_size, self.exchange = role, group, group_size, exchange
 
+    def _local_branches(self) -> List[int]:
+        if not self.cfg:
+            raise ValueError("CFG pairs need negative_prompt_embeds in set_conditions()")
+        return [0, 1] if self.group_size == 1 else [self.role]
 
-# ---------------------------------------------------------------------------- HIP defaults
-def hip_branch_forward(transformer, embeds: torch.Tensor, cond_latents: torch.Tensor,
-                       timesteps: Sequence[float], img_shapes):
-    """forward(x, i) for one CFG branch on the HIP transformer (B=1 rows)."""
-    from . import ops
-    from .scheduler import model_timesteps
-    S_noise = None
-    buf = {}
-
-    def fwd(x: torch.Tensor, i: int) -> torch.Tensor:
-        nonlocal S_noise
-        S_noise = x.shape[1]
-        inp = buf.get("inp")
-        if inp is None:
-            inp = torch.empty(x.shape[0], S_noise + cond_latents.shape[1], x.shape[2],
-                              dtype=x.dtype, device=x.device)
-            ops.copy_batched(cond_latents.expand(x.shape[0], -1, -1).contiguous(), inp[:, S_noise:])
-            buf["inp"] = inp
-        ops.copy_batched(x, inp[:, :S_noise])
-        t = model_timesteps([timesteps[i]] * x.shape[0], x.device)
-        out = transformer(inp, embeds, None, t, img_shapes, [embeds.shape[1]] * x.shape[0],
-                          return_dict=False)[0]
-        return out[:, :S_noise]
-
-    return fwd
-
-
-def hip_combine(cond: torch.Tensor, uncond: torch.Tensor, scale: float) -> torch.Tensor:
-    from . import ops
-    return ops.cfg_combine(cond.contiguous(), uncond.contiguous(), scale)
-
-
-def hip_step(dts: Sequence[float]):
-    from . import ops
-
-    def step(x: torch.Tensor, v: torch.Tensor, i: int) -> torch.Tensor:
-        out = torch.empty_like(x)
-        return ops.euler_step(x, v, [dts[i]] * x.shape[0], out)
-
-    return step
+    def _exchange(self, v_local: torch.Tensor) -> List[torch.Tensor]:
+        v_local = v_local.contiguous()
+        if self.exchange is not None:
+            parts = self.exchange(v_local)
+        else:
+            parts = [torch.empty_like(v_local) for _ in range(self.group_size)]
+            dist.all_gather(parts, v_local, group=self.group)  # pair order: [cond rank, uncond rank]
+        if self.group_size == 1:  # both branches in the one part: [cond rows; uncond rows]
+            D = self.depth
+            return [parts[0][:D], parts[0][D:]]
+        return list(parts)

@@ -97,14 +97,52 @@ class CachedConditions:
                 and self.image_key(reference_image) == self.reference_key)
 
 
-class StreamBatchDenoiser:
-    """N frames in flight, one batched DiT forward per pushed frame."""
+class HipStreamCompute:
+    """The arithmetic a stream engine needs, on the HIP path (libqie kernels behind the transformer
+    and ``ops``). The engines take any object with these methods, so their slot / exchange logic
+    also runs on the CPU with a checker's arithmetic behind it (tests, gloo)."""
 
-    def __init__(self, transformer: QwenImageTransformer2DModel, num_steps: int = 2,
+    def __init__(self, transformer: QwenImageTransformer2DModel):
+        self.tf = transformer
+        self.device = transformer.device
+
+    def empty(self, *shape) -> torch.Tensor:
+        return torch.empty(*shape, dtype=BF16, device=self.device)
+
+    def zeros(self, *shape) -> torch.Tensor:
+        return torch.zeros(*shape, dtype=BF16, device=self.device)
+
+    def timesteps(self, per_row: List[float]) -> torch.Tensor:
+        return model_timesteps(per_row, self.device)
+
+    def forward(self, inp, enc, t_rows, img_shapes, txt_lens) -> torch.Tensor:
+        return self.tf(inp, enc, None, t_rows, img_shapes, txt_lens, return_dict=False)[0]
+
+    def cfg_combine(self, cond, uncond, scale: float, out) -> torch.Tensor:
+        return ops.cfg_combine(cond, uncond, scale, out=out)
+
+    def euler_step(self, x, v, dts: List[float], out) -> None:
+        ops.euler_step(x, v, dts, out)
+
+    def copy(self, src, dst) -> None:
+        ops.copy_batched(src, dst)
+
+
+class StreamBatchDenoiser:
+    """N frames in flight, one batched DiT forward per pushed frame.
+
+    Row layout of the model input: one block of ``depth`` rows (slot k = a frame at step k) per
+    CFG branch this engine computes -- ``branches`` = [0] (cond only), or [0, 1] with true CFG
+    (cond rows then uncond rows: batched CFG). A subclass that computes a single branch and
+    exchanges the predictions with its partner (parallel.CFGPairStreamDenoiser) overrides
+    ``_local_branches`` and ``_exchange``."""
+
+    def __init__(self, transformer: Optional[QwenImageTransformer2DModel], num_steps: int = 2,
                  true_cfg_scale: float = 1.0, latent_hw: Tuple[int, int] = (64, 64),
                  cond_hw: Tuple[int, int] = (64, 64),
-                 scheduler: Optional[FlowMatchEulerDiscreteScheduler] = None):
+                 scheduler: Optional[FlowMatchEulerDiscreteScheduler] = None, compute=None):
         self.tf = transformer
+        self.cx = compute if compute is not None else HipStreamCompute(transformer)
         self.depth = int(num_steps)
         self.cfg_scale = float(true_cfg_scale)
         self.lh, self.lw = latent_hw
@@ -121,6 +159,7 @@ class StreamBatchDenoiser:
         self.timesteps = sch.timesteps.tolist()
         self.dts = [sch.dt(i) for i in range(self.depth)]
         self.cfg = False
+        self.branches: List[int] = [0]
         self.stage: List[int] = [-1] * self.depth  # -1 = empty slot
         self.frame_id: List[int] = [-1] * self.depth
         self._next_frame = 0
@@ -128,98 +167,149 @@ class StreamBatchDenoiser:
         self._enc = None
         self._txt_lens = None
         self._comb = None
-        dev = transformer.device
         self._tcache: Dict[Tuple[int, ...], torch.Tensor] = {}
         self.img_shapes = [[(1, self.lh, self.lw), (1, self.ch, self.cw)]]
 
     @property
     def rows(self) -> int:
-        return self.depth * (2 if self.cfg else 1)
+        return self.depth * len(self.branches)
+
+    def _local_branches(self) -> List[int]:
+        """CFG branches whose rows this engine computes (0 = cond, 1 = uncond)."""
+        return [0, 1] if self.cfg else [0]
 
     def set_conditions(self, prompt_embeds: torch.Tensor, prompt_embeds_mask: Optional[torch.Tensor] = None,
                        negative_prompt_embeds: Optional[torch.Tensor] = None,
                        negative_prompt_embeds_mask: Optional[torch.Tensor] = None):
-        """Cache the (padded, batched) text conditioning once per prompt."""
-        dev = self.tf.device
+        """Cache the (padded, batched) text conditioning once per prompt. Both branches' text is
+        padded to the longer of the two, whichever branches this engine computes, so a branch's
+        rows see the same shapes in every engine layout."""
+        dev = self.cx.device
         pe = prompt_embeds.to(dev, BF16)
         if pe.dim() == 2:
             pe = pe[None]
         lc = int(prompt_embeds_mask.sum()) if prompt_embeds_mask is not None else pe.shape[1]
         self.cfg = negative_prompt_embeds is not None and self.cfg_scale > 1.0
+        embeds, lens = [pe], [lc]
         if self.cfg:
             ne = negative_prompt_embeds.to(dev, BF16)
             if ne.dim() == 2:
                 ne = ne[None]
             ln = int(negative_prompt_embeds_mask.sum()) if negative_prompt_embeds_mask is not None else ne.shape[1]
-            S_txt = max(pe.shape[1], ne.shape[1])
-        else:
-            S_txt = pe.shape[1]
-        enc = torch.zeros(self.rows, S_txt, pe.shape[2], dtype=BF16, device=dev)
-        enc[: self.depth, : pe.shape[1]] = pe[0]
-        lens = [lc] * self.depth
-        if self.cfg:
-            enc[self.depth:, : ne.shape[1]] = ne[0]
-            lens += [ln] * self.depth
-        self._enc, self._txt_lens = enc, lens
-        self._inp = torch.zeros(self.rows, self.S_img, 64, dtype=BF16, device=dev)
-        self._comb = torch.empty(self.depth, self.S_noise, 64, dtype=BF16, device=dev) if self.cfg else None
-        self.stage = [-1] * self.depth
-        self.frame_id = [-1] * self.depth
+            embeds.append(ne)
+            lens.append(ln)
+        S_txt = max(e.shape[1] for e in embeds)
+        self.branches = self._local_branches()
+        D = self.depth
+        enc = self.cx.zeros(self.rows, S_txt, pe.shape[2])
+        tl: List[int] = []
+        for j, br in enumerate(self.branches):
+            enc[j * D:(j + 1) * D, : embeds[br].shape[1]] = embeds[br][0]
+            tl += [lens[br]] * D
+        self._enc, self._txt_lens = enc, tl
+        self._inp = self.cx.zeros(self.rows, self.S_img, 64)
+        self._comb = self.cx.empty(D, self.S_noise, 64) if self.cfg else None
+        self.stage = [-1] * D
+        self.frame_id = [-1] * D
 
     def _t_rows(self) -> torch.Tensor:
         st = tuple(max(s, 0) for s in self.stage)
-        t = self._tcache.get(st)
+        key = st + (len(self.branches),)
+        t = self._tcache.get(key)
         if t is None:
             per_slot = [self.timesteps[s] for s in st]
-            t = model_timesteps(per_slot * (2 if self.cfg else 1), self.tf.device)
-            self._tcache[st] = t
+            t = self.cx.timesteps(per_slot * len(self.branches))
+            self._tcache[key] = t
         return t
 
-    def push(self, noise: Optional[torch.Tensor], cond_latents: Optional[torch.Tensor]
-             ) -> Optional[Tuple[int, torch.Tensor]]:
-        """Insert a frame (packed noise [1,S_noise,64], packed cond [1,S_cond,64]);
-        run one batched forward; return (frame_id, latents [1,S_noise,64]) for
-        the frame that completed, or None while the pipeline fills.  Passing
-        ``None`` drains without inserting."""
+    def _set_slot_text(self, slot: int, embeds: List[Optional[torch.Tensor]]):
+        """Per-frame text conditioning: overwrite the text rows of ``slot`` (the reference's
+        realtime call re-encodes the prompt with every frame, qwen_realtime.py:247-255).
+        ``embeds`` = [cond, uncond]; each must fit the text length set_conditions() allocated."""
+        D, S_txt = self.depth, self._enc.shape[1]
+        for j, br in enumerate(self.branches):
+            e = embeds[br]
+            if e is None:
+                continue
+            e = e.to(self.cx.device, BF16)
+            e = e[0] if e.dim() == 3 else e
+            if e.shape[0] > S_txt:
+                raise ValueError(f"per-frame prompt has {e.shape[0]} tokens; set_conditions() sized the text "
+                                 f"rows for {S_txt}")
+            row = self._enc[j * D + slot]
+            row.zero_()
+            row[: e.shape[0]] = e
+            self._txt_lens[j * D + slot] = int(e.shape[0])
+
+    def begin(self, noise: Optional[torch.Tensor], cond_latents: Optional[torch.Tensor],
+              prompt_embeds: Optional[torch.Tensor] = None,
+              negative_prompt_embeds: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
+        """First half of push(): insert the frame and run the batched forward of this engine's
+        branches. Returns the local noise predictions [len(branches) * depth, S_noise, 64]
+        (a view of the model output), or None when no frame is in flight."""
         if self._inp is None:
             raise RuntimeError("call set_conditions() first")
-        D = self.depth
+        D, cx = self.depth, self.cx
         if noise is not None:
             slot = self.stage.index(-1) if -1 in self.stage else None
             if slot is None:
                 raise RuntimeError("no free slot (internal invariant broken)")
             inp = self._inp
-            ops.copy_batched(noise.reshape(1, self.S_noise, 64).to(BF16), inp[slot:slot + 1, : self.S_noise])
-            ops.copy_batched(cond_latents.reshape(1, self.S_cond, 64).to(BF16),
-                             inp[slot:slot + 1, self.S_noise:])
-            if self.cfg:
-                ops.copy_batched(inp[slot:slot + 1], inp[D + slot:D + slot + 1])
+            cx.copy(noise.reshape(1, self.S_noise, 64).to(BF16), inp[slot:slot + 1, : self.S_noise])
+            cx.copy(cond_latents.reshape(1, self.S_cond, 64).to(BF16), inp[slot:slot + 1, self.S_noise:])
+            for j in range(1, len(self.branches)):
+                cx.copy(inp[slot:slot + 1], inp[j * D + slot:j * D + slot + 1])
+            if prompt_embeds is not None or negative_prompt_embeds is not None:
+                self._set_slot_text(slot, [prompt_embeds, negative_prompt_embeds])
             self.stage[slot] = 0
             self.frame_id[slot] = self._next_frame
             self._next_frame += 1
         if all(s < 0 for s in self.stage):
             return None
-        out = self.tf(self._inp, self._enc, None, self._t_rows(), self.img_shapes * self.rows,
-                      self._txt_lens, return_dict=False)[0]
-        v = out[:D, : self.S_noise]
+        out = cx.forward(self._inp, self._enc, self._t_rows(), self.img_shapes * self.rows, self._txt_lens)
+        return out[:, : self.S_noise]
+
+    def _exchange(self, v_local: torch.Tensor) -> List[torch.Tensor]:
+        """[cond, uncond] predictions, each [depth, S_noise, 64]. Here both are local rows."""
+        D = self.depth
+        return [v_local[j * D:(j + 1) * D] for j in range(len(self.branches))]
+
+    def finish(self, parts: List[torch.Tensor]) -> Optional[Tuple[int, torch.Tensor]]:
+        """Second half of push(): true-CFG combine of [cond, uncond] (when on), per-row Euler
+        step, slot bookkeeping. Returns (frame_id, latents) of the frame that completed."""
+        D, cx = self.depth, self.cx
+        v = parts[0]
         if self.cfg:
-            v = ops.cfg_combine(v, out[D:, : self.S_noise], self.cfg_scale, out=self._comb)
+            v = cx.cfg_combine(parts[0], parts[1], self.cfg_scale, self._comb)
         dts = [self.dts[s] if s >= 0 else 0.0 for s in self.stage]
         x = self._inp[:D, : self.S_noise]
-        ops.euler_step(x, v, dts, x)
-        if self.cfg:
-            ops.copy_batched(self._inp[:D, : self.S_noise], self._inp[D:, : self.S_noise])
+        cx.euler_step(x, v, dts, x)
+        for j in range(1, len(self.branches)):
+            cx.copy(self._inp[:D, : self.S_noise], self._inp[j * D:(j + 1) * D, : self.S_noise])
         done = None
         for k in range(D):
             if self.stage[k] >= 0:
                 self.stage[k] += 1
                 if self.stage[k] == D:
-                    res = torch.empty(1, self.S_noise, 64, dtype=BF16, device=self.tf.device)
-                    ops.copy_batched(self._inp[k:k + 1, : self.S_noise], res)
+                    res = cx.empty(1, self.S_noise, 64)
+                    cx.copy(self._inp[k:k + 1, : self.S_noise], res)
                     done = (self.frame_id[k], res)
                     self.stage[k] = -1
                     self.frame_id[k] = -1
         return done
+
+    def push(self, noise: Optional[torch.Tensor], cond_latents: Optional[torch.Tensor],
+             prompt_embeds: Optional[torch.Tensor] = None,
+             negative_prompt_embeds: Optional[torch.Tensor] = None) -> Optional[Tuple[int, torch.Tensor]]:
+        """Insert a frame (packed noise [1,S_noise,64], packed cond [1,S_cond,64]);
+        run one batched forward; return (frame_id, latents [1,S_noise,64]) for
+        the frame that completed, or None while the pipeline fills.  Passing
+        ``None`` drains without inserting. ``prompt_embeds`` / ``negative_prompt_embeds``: this
+        frame's own text conditioning (default: the prompt given to set_conditions())."""
+        v_local = self.begin(noise, cond_latents, prompt_embeds, negative_prompt_embeds)
+        if v_local is None:
+            return None
+        return self.finish(self._exchange(v_local))
 
     def flush(self) -> List[Tuple[int, torch.Tensor]]:
         outs = []

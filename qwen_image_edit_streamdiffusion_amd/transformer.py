@@ -21,7 +21,6 @@ HBM layout per forward (B rows, S_img image tokens, S_txt text tokens):
 from __future__ import annotations
 
 import contextlib
-import os
 from collections import OrderedDict
 from dataclasses import dataclass
 from typing import Dict, Iterator, List, Optional, Sequence, Tuple
@@ -217,7 +216,8 @@ class QwenImageTransformer2DModel(nn.Module):
         # the timestep MLP, the 120 AdaLN modulation vectors and norm_out's vector depend only on
         # the weights and the per-row timesteps, which repeat every forward in the stream-batch
         # loop. Keyed on the host copy of the timestep values (scheduler.model_timesteps tags its
-        # tensors); cleared whenever weights change. False: recompute every forward (A/B switch).
+        # tensors) and on the weights' in-place version counters, and also cleared by the loaders.
+        # False: recompute every forward (A/B switch).
         self.cache_modulation = True
         self._mod_cache: "OrderedDict[tuple, tuple]" = OrderedDict()
         # K % 64 requirement of the GEMM kernels for the small input projections
@@ -354,7 +354,8 @@ class QwenImageTransformer2DModel(nn.Module):
         return self
 
     def clear_modulation_cache(self):
-        """Drop cached modulation vectors (call after changing weights outside the loaders)."""
+        """Drop cached modulation vectors. Not needed after weight changes: in-place writes change
+        the cache key (version counters) and the loaders clear it themselves."""
         self._mod_cache.clear()
 
     def _requantize_if_needed(self):
@@ -483,7 +484,12 @@ class QwenImageTransformer2DModel(nn.Module):
         host = getattr(timestep, "_qie_host", None)
         if (self.cache_modulation and self.batched_modulation and host is not None and len(host) in (1, B)
                 and timestep._version == getattr(timestep, "_qie_version", None)):
-            t_key = (tuple(host) * (B // len(host)), B)
+            # the in-place version counters of every weight the cached vectors are made from are part
+            # of the key (the per-block w_mod_* / _param_slot views share their base's counter), so a
+            # write through copy_ / a state_dict view / named_buffers misses the cache
+            t_key = (tuple(host) * (B // len(host)), B) + tuple(
+                w._version for w in (self.t_l1_w, self.t_l1_b, self.t_l2_w, self.t_l2_b, self._mod_w,
+                                     self._mod_b, self.norm_out_w, self.norm_out_b))
         if out is None:
             out = torch.empty(B, S_img, cfg.patch_size ** 2 * cfg.out_channels, dtype=BF16,
                               device=self.device)
@@ -541,9 +547,7 @@ class QwenImageTransformer2DModel(nn.Module):
         if not self.overlap_text_stream:
             return None
         if self._side is None:
-            # QIE_SIDE_PRIORITY (A/B): HIP stream priority of the text stream (lower = higher)
-            self._side = torch.cuda.Stream(device=self.device,
-                                           priority=int(os.environ.get("QIE_SIDE_PRIORITY", "0")))
+            self._side = torch.cuda.Stream(device=self.device)  # default priority, like the main stream
         return self._side
 
     def _block(self, blk: _Block, ws: _Workspace, B, S_img, S_txt, kv_len, icos, isin, tcos, tsin, eps,

@@ -52,35 +52,45 @@ def _worker_shard(rank, world, port, q):
         raise
 
 
+def _cfg_case():
+    from oracle import dit_ref as R
+    cfg = R.tiny_config()
+    params = R.random_params(cfg, seed=0)
+    g = torch.Generator().manual_seed(11)
+    pe = torch.randn(1, 12, cfg.joint_attention_dim, generator=g).to(BF16)
+    ne = torch.randn(1, 7, cfg.joint_attention_dim, generator=g).to(BF16)
+    frames = [(torch.randn(1, 16, 64, generator=g).to(BF16), torch.randn(1, 16, 64, generator=g).to(BF16))
+              for _ in range(3)]  # (noise, cond latents)
+    return R, cfg, params, pe, ne, frames
+
+
 def _worker_cfg(rank, world, port, q):
+    """parallel.CFGPairStreamDenoiser over gloo: rank 0 = cond rows, rank 1 = uncond rows of the
+    same in-flight frames; every finished frame must equal the oracle's sequential true-CFG
+    denoise of that frame, bitwise, on both ranks."""
     try:
         parallel = _init(rank, world, port)
-        from oracle import dit_ref as R
-        cfg = R.tiny_config()
-        params = R.random_params(cfg, seed=0)
-        g = torch.Generator().manual_seed(11)
-        pe = torch.randn(1, 12, cfg.joint_attention_dim, generator=g).to(BF16)
-        ne = torch.randn(1, 7, cfg.joint_attention_dim, generator=g).to(BF16)
-        cond = torch.randn(1, 16, 64, generator=g).to(BF16)
-        noise = torch.randn(1, 16, 64, generator=g).to(BF16)
+        from oracle_compute import OracleStreamCompute
+        R, cfg, params, pe, ne, frames = _cfg_case()
+        group, role, size = parallel.make_pair_groups(world)
+        assert (role, size) == (rank % 2, 2)
+        cx = OracleStreamCompute(params, cfg)
+        eng = parallel.CFGPairStreamDenoiser(None, num_steps=2, true_cfg_scale=4.0, latent_hw=(4, 4),
+                                             cond_hw=(4, 4), compute=cx, role=role, group=group)
+        eng.set_conditions(pe, None, ne)
+        assert eng.branches == [role] and eng.rows == 2
+        outs = {}
+        for noise, cond in frames:
+            r = eng.push(noise, cond)
+            if r is not None:
+                outs[r[0]] = r[1]
+        outs.update(dict(eng.flush()))
+        ok = sorted(outs) == [0, 1, 2]
         shapes = [(1, 4, 4), (1, 4, 4)]
-        sig, ts = R.sigma_schedule(2, 16)
-        emb = pe if rank % 2 == 0 else ne
-        group, role = parallel.make_pair_groups(world)
-        assert role == rank % 2
-
-        def fwd(x, i):
-            t = R.model_timestep(ts[i].expand(1))
-            out = R.transformer_forward(params, cfg, torch.cat([x, cond], 1), emb, t, shapes, [emb.shape[1]])
-            return out[:, :16].to(BF16)
-
-        den = parallel.CFGParallelDenoiser(
-            forward=fwd, combine=R.cfg_combine,
-            step=lambda x, v, i: R.euler_step(x, v, float(sig[i]), float(sig[i + 1])),
-            scale=4.0, group=group)
-        x = den.denoise(noise, 2)
-        ref = R.denoise(params, cfg, noise, cond, pe, shapes, 2, neg_embeds=ne, true_cfg_scale=4.0)
-        q.put(("ok", rank, bool(torch.equal(x, ref))))
+        for i, (noise, cond) in enumerate(frames):
+            ref = R.denoise(params, cfg, noise, cond, pe, shapes, 2, neg_embeds=ne, true_cfg_scale=4.0)
+            ok = ok and bool(torch.equal(outs[i], ref))
+        q.put(("ok", rank, ok, cx.forwards))
         dist.destroy_process_group()
     except Exception as e:
         q.put(("err", repr(e)))
@@ -107,8 +117,72 @@ def test_prompt_broadcast_and_frame_gather():
     assert outs == [[0, 1], [2, 3], [4, 5]]
 
 
-def test_cfg_parallel_pair_matches_sequential_cfg():
+def test_cfg_pair_stream_engine_matches_sequential_cfg():
     msgs = _run(_worker_cfg, n_msgs=2)
     for m in msgs:
         assert m[0] == "ok", m
         assert m[2], f"rank {m[1]} diverged from sequential true-CFG"
+        assert m[3] == 4  # 3 frames at depth 2: fill + 2 steady + 1 drain forwards per rank
+
+
+def test_cfg_pair_engine_single_process_layouts():
+    """The same engine without a process group: two engines wired together through begin() /
+    finish() (the exchange as a local list), the pair of one, and the batched-CFG stream engine all
+    give the oracle's sequential true-CFG result, bitwise."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from oracle_compute import OracleStreamCompute
+    from qwen_image_edit_streamdiffusion_amd.parallel import CFGPairStreamDenoiser
+    from qwen_image_edit_streamdiffusion_amd.stream import StreamBatchDenoiser
+    R, cfg, params, pe, ne, frames = _cfg_case()
+    shapes = [(1, 4, 4), (1, 4, 4)]
+    refs = [R.denoise(params, cfg, n, c, pe, shapes, 2, neg_embeds=ne, true_cfg_scale=4.0) for n, c in frames]
+    kw = dict(num_steps=2, true_cfg_scale=4.0, latent_hw=(4, 4), cond_hw=(4, 4))
+
+    def drive(push, flush):
+        outs = {}
+        for n, c in frames:
+            r = push(n, c)
+            if r is not None:
+                outs[r[0]] = r[1]
+        outs.update(dict(flush()))
+        return outs
+
+    # two engines, one per role, exchanging through a list
+    e = [CFGPairStreamDenoiser(None, compute=OracleStreamCompute(params, cfg), role=r,
+                               exchange=lambda v: None, **kw) for r in (0, 1)]
+    for x in e:
+        x.set_conditions(pe, None, ne)
+    both = {0: {}, 1: {}}
+
+    def push_pair(n, c):
+        v = [x.begin(n, c) for x in e]
+        if v[0] is None:
+            return None
+        parts = [t.contiguous() for t in v]
+        res = [x.finish(parts) for x in e]
+        for r in (0, 1):
+            if res[r] is not None:
+                both[r][res[r][0]] = res[r][1]
+        return None
+
+    for n, c in frames:
+        push_pair(n, c)
+    while any(s >= 0 for s in e[0].stage):
+        push_pair(None, None)
+    for r in (0, 1):
+        assert sorted(both[r]) == [0, 1, 2]
+        for i in range(3):
+            assert torch.equal(both[r][i], refs[i]), (r, i)
+    # a pair of one: both branches local, the exchange still called (returns the local part)
+    one = CFGPairStreamDenoiser(None, compute=OracleStreamCompute(params, cfg), role=0, group_size=1,
+                                exchange=lambda v: [v], **kw)
+    one.set_conditions(pe, None, ne)
+    assert one.branches == [0, 1] and one.rows == 4
+    outs = drive(one.push, one.flush)
+    assert all(torch.equal(outs[i], refs[i]) for i in range(3))
+    # the batched-CFG stream engine on the same arithmetic
+    base = StreamBatchDenoiser(None, compute=OracleStreamCompute(params, cfg), **kw)
+    base.set_conditions(pe, None, ne)
+    outs = drive(base.push, base.flush)
+    assert all(torch.equal(outs[i], refs[i]) for i in range(3))

@@ -6,7 +6,12 @@ cannot run these sizes in seconds, so the checks are:
   * the 60-block forward: finite, bitwise deterministic, and row-independent (row b of a B = 2
     forward == the same row run alone, bitwise -- what makes batched CFG equal sequential CFG);
   * the stream-batch engine (depth 2) == the serial 2-step pipeline per frame, bitwise;
-  * the VAE at 1024^2: encode and decode finite and bitwise deterministic.
+  * the VAE at 1024^2: encode and decode finite and bitwise deterministic;
+  * configs[3] (int8): exact-integer GEMMs at the headline shapes, the int8 forward's properties,
+    int8 vs bf16 under a stated bound;
+  * configs[0] (256^2 output + 1024^2 condition image) and configs[1] (4-step true CFG at 1024^2):
+    batched CFG == sequential CFG, bitwise;
+  * configs[4]'s CFG pairs: a cond and an uncond engine wired together == batched CFG, bitwise.
 Random-init weights of the real architecture (no checkpoint offline).
 """
 import math
@@ -124,3 +129,225 @@ def test_fullsize_vae_deterministic(dev):
     assert i0.dtype == torch.uint8 and i0.shape == (1, 1024, 1024, 3)
     assert torch.equal(i0, i1)
     assert 0 < i0.float().std().item()  # not a constant image
+
+
+# ---------------------------------------------------------------------------------------------
+# BASELINE configs[3]: the int8 (W8A8) path at the headline size. The reference's int8 semantics
+# are bnb LLM.int8 on the transformer (benchmark_int8.py:72-76); the build's W8A8 Int8Linear is
+# specified by oracle/int8_ref.py. Full-size checks: the exact-integer GEMM at the headline
+# shapes, and the 60-block forward's properties + its distance from the bf16 forward.
+@pytest.fixture(scope="module")
+def big8(dev, big):
+    """The int8 twin of ``big`` (same seed -> same bf16 weights, then quantised)."""
+    from qwen_image_edit_streamdiffusion_amd import QwenImageTransformer2DModel
+    m = QwenImageTransformer2DModel(num_layers=60, device=dev).random_init_(seed=0).quantize_int8()
+    for blk in m.transformer_blocks:  # keep only the int8 copies of the eight block linears
+        for n in m._I8_LINEARS:
+            setattr(blk, f"w_{n}", torch.empty(0, dtype=BF16, device=dev))
+    torch.cuda.empty_cache()
+    yield m
+    del m
+    torch.cuda.empty_cache()
+
+
+def _i8_operands(dev, M, N, K, seed):
+    g = torch.Generator(device=dev).manual_seed(seed)
+    xq = torch.randint(-127, 128, (M, K), generator=g, device=dev, dtype=torch.int8)
+    wq = torch.randint(-127, 128, (N, K), generator=g, device=dev, dtype=torch.int8)
+    sx = torch.rand(M, generator=g, device=dev) * 0.01 + 1e-3
+    sw = torch.rand(N, generator=g, device=dev) * 0.001 + 1e-4
+    b = (torch.randn(N, generator=g, device=dev) * 0.1).to(BF16)
+    return xq, wq, sx, sw, b
+
+
+def _i8_exact(xq, wq, sx, sw, b, rows):
+    """fp64 holds the int32 sums exactly: bf16(acc * sx * sw + b) on the sampled rows."""
+    acc = xq[rows].double() @ wq.double().t()
+    return (acc * sx[rows].double()[:, None] * sw.double()[None, :] + b.double()).to(BF16)
+
+
+def _sample_rows(M, n, seed):
+    edge = [0, 1, 127, 128, 255, 256, M // 2 - 1, M // 2, M - 256, M - 1]
+    rnd = torch.randint(0, M, (n,), generator=torch.Generator().manual_seed(seed)).tolist()
+    return torch.tensor(sorted(set(r for r in edge + rnd if 0 <= r < M)))
+
+
+def _close(got, ref, ulps=2, rel_l2=4e-3):
+    g, r = got.float(), ref.float()
+    assert torch.isfinite(g).all()
+    e = ((g - r).norm() / r.norm()).item()
+    assert e <= rel_l2, e
+    tol = ulps * r.abs().max().item() * 2.0 ** -8
+    assert (g - r).abs().max().item() <= tol
+
+
+@pytest.mark.parametrize("M", [16384, 432])  # image stream (B = 2 x 8192), text stream (B = 2 x 216)
+def test_int8_gemms_at_headline_shapes_exact_integer(dev, M):
+    """MLP up (N 12288, K 3072, GELU) and down (N 3072, K 12288, gated residual) of the int8 path
+    at the headline row counts, sampled rows vs the exact-integer reference."""
+    from qwen_image_edit_streamdiffusion_amd import ops
+    D, F = 3072, 12288
+    rows = _sample_rows(M, 200, 31).to(dev)
+    # up + GELU
+    xq, wq, sx, sw, b = _i8_operands(dev, M, F, D, 32)
+    ws = torch.empty(max(ops.splitk_workspace_bytes(M, F, 1) // 4, 4), device=dev)
+    y = torch.empty(M, F, dtype=BF16, device=dev)
+    if M > 1024:
+        ops.linear_i8(xq, sx, wq, sw, b, y, act=ops.ACT_GELU)
+    else:  # the text stream's launch form: unsplit tiles with the epilogue applied directly
+        ops.linear_splitk_i8(xq, sx, wq, sw, b, ops.EPI_GELU, y, ws, 1)
+    ref = torch.nn.functional.gelu(_i8_exact(xq, wq, sx, sw, b, rows).float(), approximate="tanh").to(BF16)
+    _close(y[rows], ref)
+    del xq, wq, y
+    # down + gated residual
+    B, rpb = 2, M // 2
+    xq, wq, sx, sw, b = _i8_operands(dev, M, D, F, 33)
+    g = torch.Generator(device=dev).manual_seed(34)
+    gate = (torch.randn(B, D, generator=g, device=dev) * 0.5).to(BF16)
+    resid = torch.randn(M, D, generator=g, device=dev).to(BF16)
+    r0 = resid[rows].clone()
+    if M > 1024:
+        ops.linear_gated_residual_i8(xq, sx, wq, sw, b, gate, rpb, resid)
+    else:
+        ops.linear_splitk_i8(xq, sx, wq, sw, b, ops.EPI_GATED_RESIDUAL, resid, ws, 1, gate=gate, rows_per_batch=rpb)
+    h = _i8_exact(xq, wq, sx, sw, b, rows).float()
+    gr = gate.float()[(rows // rpb)]
+    ref = (r0.float() + (gr * h).to(BF16).float()).to(BF16)
+    _close(resid[rows], ref)
+
+
+def test_fullsize_int8_forward_properties(dev, big8):
+    """60 blocks, 1024^2, B = 2, W8A8 linears: finite, bitwise deterministic, bitwise
+    row-independent (row b of the batch == that row alone with its own unpadded prompt)."""
+    hs, enc, lens = _fullsize_inputs(dev, 11)
+    t = R.model_timestep(torch.tensor([1000.0, 20.0])).to(dev)
+    a = big8(hs, enc, None, t, [SHAPES] * 2, lens, return_dict=False)[0].clone()
+    b = big8(hs, enc, None, t, [SHAPES] * 2, lens, return_dict=False)[0].clone()
+    assert a.shape == (2, S_IMG, 64) and torch.isfinite(a.float()).all()
+    assert torch.equal(a, b)
+    for r in range(2):
+        one = big8(hs[r:r + 1], enc[r:r + 1, :lens[r]], None, t[r:r + 1], [SHAPES], lens[r:r + 1],
+                   return_dict=False)[0]
+        assert torch.equal(one, a[r:r + 1]), (r, rel(one, a[r:r + 1]))
+
+
+INT8_VS_BF16_FORWARD = 6e-2   # rel-L2 of one 60-block forward's prediction
+INT8_VS_BF16_LATENTS = 6e-2   # rel-L2 of the latents after the 2-step stream
+
+
+def test_fullsize_int8_vs_bf16_bound(dev, big, big8):
+    """The int8 model against the bf16 model of the same weights: one forward, and the latents of
+    three frames after the depth-2 stream engine (the headline loop). Random-init N(0, 0.02)
+    weights of the real architecture; the bounds are stated above (measured ~2x below them)."""
+    from qwen_image_edit_streamdiffusion_amd import StreamBatchDenoiser
+    hs, enc, lens = _fullsize_inputs(dev, 14)
+    t = R.model_timestep(torch.tensor([1000.0, 20.0])).to(dev)
+    a = big(hs, enc, None, t, [SHAPES] * 2, lens, return_dict=False)[0]
+    b = big8(hs, enc, None, t, [SHAPES] * 2, lens, return_dict=False)[0]
+    e = rel(b[:, :4096], a[:, :4096])
+    print(f"int8 vs bf16, one forward: rel-L2 {e:.3e}", flush=True)
+    assert e <= INT8_VS_BF16_FORWARD, e
+    g = torch.Generator(device=dev).manual_seed(15)
+    pe = torch.randn(1, S_TXT, 3584, generator=g, device=dev).to(BF16)
+    frames = [torch.randn(1, 4096, 64, generator=g, device=dev).to(BF16) for _ in range(3)]
+    noises = [torch.randn(1, 4096, 64, generator=g, device=dev).to(BF16) for _ in range(3)]
+    outs = []
+    for m in (big, big8):
+        eng = StreamBatchDenoiser(m, num_steps=2, latent_hw=(64, 64), cond_hw=(64, 64))
+        eng.set_conditions(pe)
+        o = {}
+        for n, f in zip(noises, frames):
+            r = eng.push(n, f)
+            if r is not None:
+                o[r[0]] = r[1].clone()
+        o.update({k: v.clone() for k, v in eng.flush()})
+        outs.append(o)
+    for i in range(3):
+        e = rel(outs[1][i], outs[0][i])
+        print(f"int8 vs bf16, frame {i} latents after 2 steps: rel-L2 {e:.3e}", flush=True)
+        assert torch.isfinite(outs[1][i].float()).all() and e <= INT8_VS_BF16_LATENTS, (i, e)
+
+
+# ---------------------------------------------------------------------------------------------
+# BASELINE configs[0] and configs[1] at their stated sizes, and configs[4]'s CFG pairs.
+def test_config0_256_output_batched_cfg_equals_sequential(dev, big):
+    """configs[0] on the HIP path: 256x256 output (16 x 16 = 256 noise tokens) with the 1024^2-area
+    condition image Edit-Plus always encodes (4096 tokens), 216 / 211 text tokens: S = 4568,
+    S_pad = 4608; 60 blocks at full width, 2 steps, true CFG. Finite, and batched CFG equals the
+    two sequential forwards bit for bit."""
+    from qwen_image_edit_streamdiffusion_amd import QwenImageEditPlusPipeline
+    g = torch.Generator(device=dev).manual_seed(16)
+    pe = torch.randn(1, S_TXT, 3584, generator=g, device=dev).to(BF16)
+    ne = torch.randn(1, S_TXT - 5, 3584, generator=g, device=dev).to(BF16)
+    cond = torch.randn(1, 4096, 64, generator=g, device=dev).to(BF16)
+    noise = torch.randn(1, 256, 64, generator=g, device=dev).to(BF16)
+    pipe = QwenImageEditPlusPipeline(big)
+    kw = dict(prompt_embeds=pe, negative_prompt_embeds=ne, image_latents=cond, latents=noise, true_cfg_scale=4.0,
+              num_inference_steps=2, height=256, width=256, cond_shape=(64, 64), output_type="latent")
+    a = pipe(batched_cfg=True, **kw).images
+    b = pipe(batched_cfg=False, **kw).images
+    assert a.shape == (1, 256, 64) and torch.isfinite(a.float()).all()
+    assert torch.equal(a, b), rel(a, b)
+    assert not torch.equal(a, noise)
+
+
+def test_config1_four_step_true_cfg_batched_equals_sequential(dev, big):
+    """configs[1]: 4-step true-CFG 4.0 at 1024^2, cond + uncond batched in one B = 2 forward per
+    step == the reference's two sequential forwards per step, bitwise (60 blocks)."""
+    from qwen_image_edit_streamdiffusion_amd import QwenImageEditPlusPipeline
+    g = torch.Generator(device=dev).manual_seed(17)
+    pe = torch.randn(1, S_TXT, 3584, generator=g, device=dev).to(BF16)
+    ne = torch.randn(1, S_TXT - 5, 3584, generator=g, device=dev).to(BF16)
+    cond = torch.randn(1, 4096, 64, generator=g, device=dev).to(BF16)
+    noise = torch.randn(1, 4096, 64, generator=g, device=dev).to(BF16)
+    pipe = QwenImageEditPlusPipeline(big)
+    kw = dict(prompt_embeds=pe, negative_prompt_embeds=ne, image_latents=cond, latents=noise, true_cfg_scale=4.0,
+              num_inference_steps=4, height=1024, width=1024, output_type="latent")
+    a = pipe(batched_cfg=True, **kw).images
+    b = pipe(batched_cfg=False, **kw).images
+    assert torch.isfinite(a.float()).all()
+    assert torch.equal(a, b), rel(a, b)
+
+
+def test_fullsize_cfg_pair_engines_equal_batched_cfg(dev, big):
+    """configs[4]'s CFG axis on the HIP path in one process: a cond engine and an uncond engine
+    (parallel.CFGPairStreamDenoiser, roles 0 / 1) exchanging their predictions through a local
+    list give, on both sides, exactly the latents of the batched-CFG stream engine (B = 4)."""
+    from qwen_image_edit_streamdiffusion_amd import StreamBatchDenoiser
+    from qwen_image_edit_streamdiffusion_amd.parallel import CFGPairStreamDenoiser
+    g = torch.Generator(device=dev).manual_seed(18)
+    pe = torch.randn(1, S_TXT, 3584, generator=g, device=dev).to(BF16)
+    ne = torch.randn(1, S_TXT - 5, 3584, generator=g, device=dev).to(BF16)
+    frames = [(torch.randn(1, 4096, 64, generator=g, device=dev).to(BF16),
+               torch.randn(1, 4096, 64, generator=g, device=dev).to(BF16)) for _ in range(3)]
+    kw = dict(num_steps=2, true_cfg_scale=4.0, latent_hw=(64, 64), cond_hw=(64, 64))
+    base = StreamBatchDenoiser(big, **kw)
+    base.set_conditions(pe, None, ne)
+    ref = {}
+    for n, c in frames:
+        r = base.push(n, c)
+        if r is not None:
+            ref[r[0]] = r[1].clone()
+    ref.update({k: v.clone() for k, v in base.flush()})
+    eng = [CFGPairStreamDenoiser(big, role=r, exchange=lambda v: None, **kw) for r in (0, 1)]
+    for e in eng:
+        e.set_conditions(pe, None, ne)
+    assert [e.rows for e in eng] == [2, 2]
+    got = {0: {}, 1: {}}
+
+    def push_pair(n, c):
+        v = [e.begin(n, c) for e in eng]
+        parts = [x.clone() for x in v]  # the gather: each side receives copies of both predictions
+        for r in (0, 1):
+            res = eng[r].finish(parts)
+            if res is not None:
+                got[r][res[0]] = res[1].clone()
+
+    for n, c in frames:
+        push_pair(n, c)
+    while any(s >= 0 for s in eng[0].stage):
+        push_pair(None, None)
+    for r in (0, 1):
+        assert sorted(got[r]) == [0, 1, 2]
+        for i in range(3):
+            assert torch.equal(got[r][i], ref[i]), (r, i, rel(got[r][i], ref[i]))

@@ -311,3 +311,151 @@ def test_modulation_cache_bitwise_and_invalidated(dev, tiny):
     m.cache_modulation = True
     assert torch.equal(run(ta), ref_new) and torch.equal(run(ta), ref_new)
     assert not torch.equal(ref_new, ref_a)
+    # an in-place write outside the loaders (no clear_modulation_cache call) must miss the cache:
+    # the weights' version counters are part of the key
+    with torch.no_grad():
+        m._param_slot("transformer_blocks.1.txt_mod.1.bias").add_(0.25)
+        m.norm_out_w.mul_(1.5)
+    m.cache_modulation = False
+    ref_inplace = run(ta)
+    m.cache_modulation = True
+    assert torch.equal(run(ta), ref_inplace) and torch.equal(run(ta), ref_inplace)
+    assert not torch.equal(ref_inplace, ref_new)
+
+
+def test_cfg_pair_engine_layouts_equal_batched_cfg(dev, tiny):
+    """parallel.CFGPairStreamDenoiser on the HIP path, single process: a pair of one (both branches
+    local, the exchange still taken) and two engines wired through begin() / finish() both equal
+    the batched-CFG stream engine bit for bit."""
+    cfg, params, m = tiny
+    from qwen_image_edit_streamdiffusion_amd import StreamBatchDenoiser
+    from qwen_image_edit_streamdiffusion_amd.parallel import CFGPairStreamDenoiser
+    g = torch.Generator().manual_seed(51)
+    pe = torch.randn(1, 20, cfg.joint_attention_dim, generator=g).to(BF16).to(dev)
+    ne = torch.randn(1, 13, cfg.joint_attention_dim, generator=g).to(BF16).to(dev)
+    frames = [(torch.randn(1, 64, 64, generator=g).to(BF16).to(dev),
+               torch.randn(1, 64, 64, generator=g).to(BF16).to(dev)) for _ in range(4)]
+    kw = dict(num_steps=2, true_cfg_scale=4.0, latent_hw=(8, 8), cond_hw=(8, 8))
+
+    def drive(eng):
+        outs = {}
+        for n, c in frames:
+            r = eng.push(n, c)
+            if r is not None:
+                outs[r[0]] = r[1].clone()
+        outs.update({k: v.clone() for k, v in eng.flush()})
+        return outs
+
+    base = StreamBatchDenoiser(m, **kw)
+    base.set_conditions(pe, None, ne)
+    ref = drive(base)
+    one = CFGPairStreamDenoiser(m, role=0, group_size=1, exchange=lambda v: [v.clone()], **kw)
+    one.set_conditions(pe, None, ne)
+    assert one.rows == 4
+    got = drive(one)
+    assert sorted(got) == [0, 1, 2, 3] and all(torch.equal(got[i], ref[i]) for i in range(4))
+    eng = [CFGPairStreamDenoiser(m, role=r, exchange=lambda v: None, **kw) for r in (0, 1)]
+    for e in eng:
+        e.set_conditions(pe, None, ne)
+    both = {0: {}, 1: {}}
+
+    def push_pair(n, c):
+        parts = [e.begin(n, c).clone() for e in eng]
+        for r in (0, 1):
+            res = eng[r].finish(parts)
+            if res is not None:
+                both[r][res[0]] = res[1].clone()
+
+    for n, c in frames:
+        push_pair(n, c)
+    while any(s >= 0 for s in eng[0].stage):
+        push_pair(None, None)
+    for r in (0, 1):
+        assert all(torch.equal(both[r][i], ref[i]) for i in range(4)), r
+    with pytest.raises(ValueError):
+        CFGPairStreamDenoiser(m, role=0, group_size=1, exchange=lambda v: [v], **dict(kw, true_cfg_scale=1.0))
+
+
+def test_stream_per_frame_prompt_equals_serial(dev, tiny):
+    """Every frame with its own prompt embedding (the reference's realtime call re-encodes the
+    prompt with each camera frame, qwen_realtime.py:247-255): the stream engine's per-slot text
+    rows give each frame exactly the serial pipeline's result for ITS embedding -- lengths differ
+    per frame, so rows of one forward carry different valid text lengths."""
+    cfg, params, m = tiny
+    from qwen_image_edit_streamdiffusion_amd import StreamBatchDenoiser
+    pipe = _pipe(m)
+    g = torch.Generator().manual_seed(52)
+    lens = [20, 17, 20, 11]
+    pes = [torch.randn(1, n, cfg.joint_attention_dim, generator=g).to(BF16).to(dev) for n in lens]
+    ne = torch.randn(1, 13, cfg.joint_attention_dim, generator=g).to(BF16).to(dev)
+    frames = [torch.randn(1, 64, 64, generator=g).to(BF16).to(dev) for _ in range(4)]
+    noises = [torch.randn(1, 64, 64, generator=g).to(BF16).to(dev) for _ in range(4)]
+    for cfg_scale in (1.0, 4.0):
+        eng = StreamBatchDenoiser(m, num_steps=2, true_cfg_scale=cfg_scale, latent_hw=(8, 8), cond_hw=(8, 8))
+        eng.set_conditions(pes[0], None, ne if cfg_scale > 1 else None)
+        outs = {}
+        for i in range(4):
+            r = eng.push(noises[i], frames[i], prompt_embeds=pes[i])
+            if r is not None:
+                outs[r[0]] = r[1].clone()
+        outs.update({k: v.clone() for k, v in eng.flush()})
+        for i in range(4):
+            ser = pipe(prompt_embeds=pes[i], negative_prompt_embeds=ne if cfg_scale > 1 else None,
+                       image_latents=frames[i], latents=noises[i], true_cfg_scale=cfg_scale,
+                       num_inference_steps=2, height=128, width=128, output_type="latent").images
+            assert torch.equal(outs[i], ser), (cfg_scale, i, rel(outs[i], ser))
+    with pytest.raises(ValueError):  # longer than the text rows set_conditions() sized
+        eng.push(noises[0], frames[0], prompt_embeds=torch.zeros(1, 21, cfg.joint_attention_dim, dtype=BF16, device=dev))
+
+
+def test_realtime_latent_cache_through_stream_engine(dev, tiny):
+    """qwen_realtime.py:201-224 prepare_latent (never called by the reference's own loop): fresh
+    noise on keyframes (every ``keyframe_interval`` frames, and while no frame has completed),
+    otherwise the last completed latent + noise_strength * noise. Through QwenRealtimePipeline and
+    the stream engine: the latents each frame started from follow that rule with the pipeline's
+    generator stream, and every finished frame equals the serial 2-step pipeline run from the same
+    start latents, bitwise."""
+    cfg, params, m = tiny
+    from qwen_image_edit_streamdiffusion_amd import QwenRealtimePipeline, StreamConfig
+    sc = StreamConfig(num_inference_steps=2, true_cfg_scale=1.0, noise_strength=0.05, keyframe_interval=3,
+                      output_size=(128, 128), cond_size=(128, 128), use_prev_latent=True)
+    rt = QwenRealtimePipeline(sc)
+    rt.load_model(transformer=m)
+    g = torch.Generator().manual_seed(53)
+    pe = torch.randn(1, 20, cfg.joint_attention_dim, generator=g).to(BF16).to(dev)
+    rt.precompute_conditions("a prompt", prompt_embeds=pe)
+    conds = [torch.randn(1, 64, 64, generator=g).to(BF16).to(dev) for _ in range(7)]
+    starts, keyflags, prevs = [], [], []
+    orig = rt.prepare_latent
+
+    def spy(cond):
+        prevs.append(None if rt.prev_latent is None else rt.prev_latent.clone())
+        x = orig(cond)
+        starts.append(x.clone())
+        keyflags.append(rt.is_keyframe)
+        return x
+
+    rt.prepare_latent = spy
+    done = []
+    for c in conds:
+        out = rt.process_frame(c)
+        if out is not None:
+            done.append(out.clone())
+    done += [lat.clone() for _, lat in rt.engine.flush()]
+    assert len(done) == 7
+    # the rule, replayed with the same generator stream (seed 42 on the device, load_model)
+    gen = torch.Generator(device=dev).manual_seed(42)
+    assert keyflags == [True, True, False, True, False, False, True]  # no finished frame yet at frame 1
+    for i in range(7):
+        noise = torch.randn((1, 64, 64), generator=gen, device=dev, dtype=BF16)
+        if keyflags[i]:
+            exp = noise
+        else:
+            assert prevs[i] is not None and torch.equal(prevs[i], done[i - 2])  # depth 2: frame i-2 is the last finished
+            exp = (prevs[i].float() + 0.05 * noise.float()).to(BF16)
+        assert torch.equal(starts[i], exp), i
+    pipe = _pipe(m)
+    for i in range(7):
+        ser = pipe(prompt_embeds=pe, image_latents=conds[i], latents=starts[i], true_cfg_scale=1.0,
+                   num_inference_steps=2, height=128, width=128, output_type="latent").images
+        assert torch.equal(done[i], ser), (i, rel(done[i], ser))
