@@ -6,20 +6,11 @@ the diffusers ``QwenImageTransformer2DModel`` module surface, the
 qwen_realtime stream-batch loop -- all arithmetic in hand-written HIP kernels
 (libqie.so, include/qie.h) loaded through a thin C ABI.
 """
-import os as _os
-
-# The transformer overlaps its text stream with the image stream on a second HIP stream; once RCCL
-# adds its own streams (parallel.py), HIP's default 4 hardware queues per process make the two
-# model streams share a queue and the overlap serialises (~9 % per step). Effective only when this
-# package is imported before HIP initialises; parallel.init_distributed warns otherwise.
-if int(_os.environ.get("GPU_MAX_HW_QUEUES") or 0) < 8:  # raise an inherited 4, keep a larger value
-    _os.environ["GPU_MAX_HW_QUEUES"] = "8"
-
-from ._lib import QieError, load as load_library  # noqa: E402
-from .transformer import QwenImageTransformer2DModel, TransformerConfig  # noqa: E402
-from .scheduler import FlowMatchEulerDiscreteScheduler, calculate_shift  # noqa: E402
-from .pipeline import QwenImageEditPlusPipeline, calculate_dimensions  # noqa: E402
-from .stream import StreamConfig, CachedConditions, StreamBatchDenoiser, QwenRealtimePipeline  # noqa: E402
+from ._lib import QieError, load as load_library
+from .transformer import QwenImageTransformer2DModel, TransformerConfig
+from .scheduler import FlowMatchEulerDiscreteScheduler, calculate_shift
+from .pipeline import QwenImageEditPlusPipeline, calculate_dimensions
+from .stream import StreamConfig, CachedConditions, StreamBatchDenoiser, QwenRealtimePipeline
 
 __all__ = [
     "QieError", "load_library", "QwenImageTransformer2DModel", "TransformerConfig",

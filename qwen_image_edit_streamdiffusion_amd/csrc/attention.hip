@@ -446,9 +446,9 @@ __global__ void __launch_bounds__(256) attn_combine_kernel(AttnArgs a) {
     const float mc = pml[pi * 2], lc = pml[pi * 2 + 1];
     const float w = mc == -INFINITY ? 0.f : __builtin_amdgcn_exp2f((mc - mx) * a.c);
     const f32x2_t ov = *(const f32x2_t*)(a.ws + pi * kDh + 2 * lane);
-    l += w * lc;
-    o0 += w * ov[0];
-    o1 += w * ov[1];
+    l = __builtin_fmaf(w, lc, l);
+    o0 = __builtin_fmaf(w, ov[0], o0);
+    o1 = __builtin_fmaf(w, ov[1], o1);
   }
   const float inv = 1.0f / l;
   *(uint32_t*)(dst + 2 * lane) = pack2(o0 * inv, o1 * inv);

@@ -115,7 +115,7 @@ __global__ void __launch_bounds__(256)
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float d = f[j] - mean;
-        sq += d * d;
+        sq = __builtin_fmaf(d, d, sq);
       }
     }
   const float rstd = rsqrtf(wave_sum(sq) / (float)D + eps);
@@ -209,7 +209,7 @@ __global__ void __launch_bounds__(256)
     if (c < nch) {
       unpack8(*(const u32x4_t*)(xr + c * 8), v[i]);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) sq += v[i][j] * v[i][j];
+      for (int j = 0; j < 8; ++j) sq = __builtin_fmaf(v[i][j], v[i][j], sq);
     }
   }
   const float rstd = rsqrtf(wave_sum(sq) / (float)D + eps);
@@ -244,7 +244,7 @@ __global__ void __launch_bounds__(256)
   unpack8(*(const u32x4_t*)p, v);
   float sq = 0.f;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) sq += v[j] * v[j];
+  for (int j = 0; j < 8; ++j) sq = __builtin_fmaf(v[j], v[j], sq);
   sq = group_sum<16>(sq);
   const float rstd = rsqrtf(sq * (1.0f / 128.0f) + eps);
   float w8[8];
@@ -257,8 +257,8 @@ __global__ void __launch_bounds__(256)
   for (int j = 0; j < 4; ++j) {
     const float a = rbf(rbf(v[2 * j] * rstd) * w8[2 * j]);
     const float bb = rbf(rbf(v[2 * j + 1] * rstd) * w8[2 * j + 1]);
-    o[2 * j] = (a * cs[j] - bb * sn[j]) * osc;
-    o[2 * j + 1] = (a * sn[j] + bb * cs[j]) * osc;
+    o[2 * j] = __builtin_fmaf(a, cs[j], -(bb * sn[j])) * osc;
+    o[2 * j + 1] = __builtin_fmaf(a, sn[j], bb * cs[j]) * osc;
   }
   *(u32x4_t*)p = pack8(o);
 }

@@ -46,8 +46,8 @@ __global__ void __launch_bounds__(256)
       const float u = bf2f(unc[(int64_t)row * C + ch]);
       cb[i] = c;
       comb[i] = rbf(u + rbf(s * rbf(c - u)));
-      cn += c * c;
-      nn += comb[i] * comb[i];
+      cn = __builtin_fmaf(c, c, cn);
+      nn = __builtin_fmaf(comb[i], comb[i], nn);
     }
   }
   cn = rbf(sqrtf(wave_sum(cn)));

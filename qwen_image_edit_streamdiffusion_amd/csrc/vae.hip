@@ -128,7 +128,7 @@ __global__ void __launch_bounds__(256)
     const float tm = fmaxf(fmaxf(t[0], t[1]), fmaxf(t[2], t[3])) * scale;
     float tl = 0.f;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) tl += __expf(t[k] * scale - tm);
+    for (int k = 0; k < 4; ++k) tl += __expf(__builtin_fmaf(t[k], scale, -tm));
     ml_merge(m, l, tm, tl);
   }
 #pragma unroll

@@ -271,10 +271,10 @@ __global__ void __launch_bounds__(256)
     const float ms = mlpart[((int64_t)s * P + q) * 2], ls = mlpart[((int64_t)s * P + q) * 2 + 1];
     if (ms == -INFINITY) continue;
     const float w = exp2f(ms - mx);
-    den += ls * w;
+    den = __builtin_fmaf(ls, w, den);
     const f32x4_t v = *(const f32x4_t*)(opart + ((int64_t)s * P + q) * kC + d);
 #pragma unroll
-    for (int k = 0; k < 4; ++k) acc[k] += v[k] * w;
+    for (int k = 0; k < 4; ++k) acc[k] = __builtin_fmaf(v[k], w, acc[k]);
   }
   const float inv = den > 0.f ? 1.0f / den : 0.f;
   *(u32x2_t*)(out + (int64_t)q * ldo + d) = u32x2_t{pack2(acc[0] * inv, acc[1] * inv), pack2(acc[2] * inv, acc[3] * inv)};

@@ -17,6 +17,7 @@ import io
 import multiprocessing as mp
 import queue
 import threading
+import time
 from concurrent.futures import ThreadPoolExecutor
 from typing import List, Optional
 
@@ -61,7 +62,8 @@ def _worker_main(rank: int, device_index: Optional[int], loader_spec: str, do_wa
 
 
 class WorkerDied(RuntimeError):
-    """The GPU worker serving a request exited (GPU fault, OOM kill) before it answered."""
+    """The GPU worker serving a request exited (GPU fault, OOM kill) before it answered, or was
+    terminated because the request passed its deadline (a hung worker)."""
 
 
 class GpuDispatcher:
@@ -75,11 +77,15 @@ class GpuDispatcher:
     ``errors``, and a fresh ``spawn`` child is started for that GPU in the background (a new
     process, never an exec of this one). The slot stays out of the free list until the new worker
     reports ready, so a lost GPU never turns into a permanent 429.
+
+    ``request_timeout`` (seconds, None = no deadline): a worker that is alive but has not answered
+    by then (a stuck kernel, a deadlock) is terminated and takes the same path as a dead one --
+    the request fails with ``WorkerDied`` and a fresh worker is spawned for the slot.
     """
 
     def __init__(self, size: int, loader_spec: str, devices: Optional[List[Optional[int]]] = None,
                  do_warmup: bool = True, start_timeout: float = 1800.0, poll: float = 1.0,
-                 respawn: bool = True):
+                 respawn: bool = True, request_timeout: Optional[float] = None):
         self.size = size
         self.loader_spec = loader_spec
         self.devices = list(devices) if devices is not None else list(range(size))
@@ -87,6 +93,7 @@ class GpuDispatcher:
         self.start_timeout = start_timeout
         self.poll = poll
         self.respawn = respawn
+        self.request_timeout = request_timeout
         self.executor = ThreadPoolExecutor(max_workers=size)
         self._lock = threading.Lock()
         self._free: List[int] = []
@@ -157,11 +164,11 @@ class GpuDispatcher:
                 self._down.discard(token)
                 self._free.append(token)
 
-    def _worker_died(self, token: int):
+    def _worker_died(self, token: int, why: Optional[str] = None):
         code = self._procs[token].exitcode
         with self._lock:
             self._down.add(token)
-        self.errors[token] = f"worker {token} died (exit code {code})"
+        self.errors[token] = why or f"worker {token} died (exit code {code})"
         try:
             self._procs[token].join(timeout=1)
         except Exception:
@@ -173,6 +180,7 @@ class GpuDispatcher:
     def run(self, token: int, image: Image.Image, req) -> Image.Image:
         self._req[token].put((_to_png(image), req.prompt, req.steps, req.use_cfg))
         res, proc = self._res[token], self._procs[token]
+        deadline = None if self.request_timeout is None else time.monotonic() + self.request_timeout
         while True:
             try:
                 kind, _, payload = res.get(timeout=self.poll)
@@ -184,6 +192,16 @@ class GpuDispatcher:
                         break
                     except queue.Empty:
                         self._worker_died(token)
+                if deadline is not None and time.monotonic() > deadline:
+                    # alive but silent past the deadline: end it (SIGTERM, then SIGKILL) and take
+                    # the dead-worker path, which spawns a replacement
+                    proc.terminate()
+                    proc.join(timeout=5)
+                    if proc.is_alive():
+                        proc.kill()
+                        proc.join(timeout=5)
+                    self._worker_died(token, f"worker {token} died: no answer within {self.request_timeout:g} s "
+                                             "(terminated)")
         if kind != "ok":
             raise RuntimeError(payload)
         return _from_png(payload)

@@ -28,6 +28,19 @@ import torch.distributed as dist
 from .stream import StreamBatchDenoiser
 
 
+def raise_hip_hw_queues(n: int = 8) -> bool:
+    """Explicit opt-in for launchers of multi-rank runs (bench.py does the same inline): raise
+    GPU_MAX_HW_QUEUES to ``n`` for this process and its children. Once RCCL adds its streams, HIP's
+    default 4 hardware queues make the transformer's two streams share a queue and its text-stream
+    overlap serialises (~9 % per step). Only effective before the first HIP call; returns False
+    (and changes nothing) when HIP is already initialised. Importing the package never does this."""
+    if torch.cuda.is_initialized():
+        return False
+    if int(os.environ.get("GPU_MAX_HW_QUEUES") or 0) < n:
+        os.environ["GPU_MAX_HW_QUEUES"] = str(n)
+    return True
+
+
 def init_distributed(backend: Optional[str] = None):
     """Read RANK/WORLD_SIZE/LOCAL_RANK (torch.distributed.run), init the process
     group if world > 1, return (rank, world, local_rank, device)."""
@@ -37,7 +50,8 @@ def init_distributed(backend: Optional[str] = None):
     if world > 1 and torch.cuda.is_initialized() and int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 8:
         warnings.warn("HIP initialised with fewer than 8 hardware queues: RCCL's streams will share "
                       "them with the transformer's text-stream overlap, which then serialises (~9 % "
-                      "per step); export GPU_MAX_HW_QUEUES=8 before the first HIP call")
+                      "per step); export GPU_MAX_HW_QUEUES=8 (or call parallel.raise_hip_hw_queues()) "
+                      "before the first HIP call")
     use_cuda = torch.cuda.is_available() and backend != "gloo"
     device = torch.device("cuda", local) if use_cuda else torch.device("cpu")
     if use_cuda:

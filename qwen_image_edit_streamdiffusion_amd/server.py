@@ -19,7 +19,7 @@ the busy gate only answers 429 when every GPU is busy.
 
 Run: ``python -m qwen_image_edit_streamdiffusion_amd.server`` (env ``QIE_MODEL_PATH``,
 ``QIE_LORA_PATH``, ``QIE_LORA_WEIGHT``, ``QIE_INT8``, ``QIE_ENCODERS=module:factory``,
-``QIE_WORKERS``, ``QIE_PORT`` = 8086).
+``QIE_WORKERS``, ``QIE_REQUEST_TIMEOUT`` (seconds, multi-worker only), ``QIE_PORT`` = 8086).
 """
 from __future__ import annotations
 
@@ -268,7 +268,9 @@ def main():
     dispatcher = None
     if n > 1:
         from .dispatch import GpuDispatcher
-        dispatcher = GpuDispatcher(n, "qwen_image_edit_streamdiffusion_amd.server:load_pipeline_from_env")
+        rt = os.environ.get("QIE_REQUEST_TIMEOUT")  # seconds; a worker silent for longer is replaced
+        dispatcher = GpuDispatcher(n, "qwen_image_edit_streamdiffusion_amd.server:load_pipeline_from_env",
+                                   request_timeout=float(rt) if rt else None)
     app = create_app(dispatcher=dispatcher)
     uvicorn.run(app, host=os.environ.get("QIE_HOST", "0.0.0.0"), port=int(os.environ.get("QIE_PORT", "8086")))
 

@@ -81,9 +81,9 @@ class CachedConditions:
             return None
         import hashlib
         h = hashlib.sha1()
-        if isinstance(image, torch.Tensor):
-            h.update(str(tuple(image.shape)).encode())
-            h.update(image.detach().cpu().contiguous().numpy().tobytes())
+        if isinstance(image, torch.Tensor):  # raw bytes: numpy has no bfloat16
+            h.update(f"{tuple(image.shape)}{image.dtype}".encode())
+            h.update(image.detach().contiguous().view(-1).view(torch.uint8).cpu().numpy().tobytes())
         else:
             im = image.convert("RGB")
             h.update(str(im.size).encode())

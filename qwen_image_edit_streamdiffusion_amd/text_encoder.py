@@ -361,7 +361,8 @@ class QwenVLEncoder:
 def _image_digest(im) -> str:
     """Content key of a condition image (PIL or tensor) for the prompt-embedding cache."""
     if torch.is_tensor(im):
-        data, tag = im.detach().cpu().contiguous().numpy().tobytes(), (tuple(im.shape), str(im.dtype))
+        data = im.detach().contiguous().view(-1).view(torch.uint8).cpu().numpy().tobytes()  # any dtype, bf16 too
+        tag = (tuple(im.shape), str(im.dtype))
     else:
         data, tag = im.tobytes(), (im.size, im.mode)
     return hashlib.blake2b(repr(tag).encode() + data, digest_size=16).hexdigest()

@@ -3,6 +3,8 @@ RoPE tables, pipeline dimension rules, diffusers state_dict packing, LoRA fuse,
 host-side argument validation, and the stream-batch slot bookkeeping (with the
 device ops replaced by CPU stand-ins, test-only)."""
 import numpy as np
+import os
+
 import pytest
 import torch
 
@@ -296,6 +298,25 @@ def test_prompt_cache_keys_on_reference_image():
     assert not c.is_valid("p", a)
     c.reference_key = c.image_key(a)
     assert c.is_valid("p", Image.new("RGB", (8, 8), "red")) and not c.is_valid("p", b)
+    # tensor images of any dtype (numpy has no bfloat16): keyed on shape, dtype and raw bytes
+    tb = torch.arange(48, dtype=torch.float32).view(4, 4, 3).to(torch.bfloat16)
+    k = c.image_key(tb)
+    assert k == c.image_key(tb.clone()) and k != c.image_key(tb + 1) and k != c.image_key(tb.float())
+    assert c.image_key(tb.view(2, 8, 3)) != k
+
+
+def test_importing_the_package_leaves_the_environment_alone():
+    """The HIP hardware-queue setting belongs to the launchers (bench.py, parallel.raise_hip_hw_queues),
+    not to `import`: a fresh interpreter's environment is the same before and after the import."""
+    import subprocess
+    import sys
+    code = ("import os; a = dict(os.environ); import qwen_image_edit_streamdiffusion_amd; "
+            "import qwen_image_edit_streamdiffusion_amd.parallel as p; assert dict(os.environ) == a; "
+            "assert p.raise_hip_hw_queues(8) and os.environ['GPU_MAX_HW_QUEUES'] == '8'")
+    env = dict(os.environ, GPU_MAX_HW_QUEUES="4")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", code], env=env, cwd=root, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-2000:]
 
 
 def test_text_split_rule_and_per_linear_config():

@@ -172,3 +172,25 @@ def test_gpu_dispatcher_worker_death_is_500_and_respawned():
         assert d.restarts == 1 and not d.errors
         r = c.post("/edit", json={"image": b64_png(solid("gray")), "prompt": "ok"})
         assert r.status_code == 200
+
+
+def test_gpu_dispatcher_hung_worker_hits_deadline_and_is_respawned():
+    """A worker that stays alive but never answers: the request fails with 500 once its deadline
+    passes, the worker is terminated, and a fresh one takes the slot (no permanent 429)."""
+    import time
+    from qwen_image_edit_streamdiffusion_amd.dispatch import GpuDispatcher
+    d = GpuDispatcher(1, "server_stubs:load_hanging_stub", devices=[None], do_warmup=False,
+                      start_timeout=300, poll=0.2, request_timeout=1.5)
+    with TestClient(S.create_app(dispatcher=d)) as c:
+        t0 = time.time()
+        r = c.post("/edit", json={"image": b64_png(solid("gray")), "prompt": "hang"})
+        assert r.status_code == 500 and "no answer within" in r.json()["detail"]
+        assert time.time() - t0 < 30
+        for _ in range(600):
+            if d.restarts == 1 and not d.errors and d.try_acquire() is not None:
+                d.release(0)
+                break
+            time.sleep(0.1)
+        assert d.restarts == 1 and not d.errors
+        r = c.post("/edit", json={"image": b64_png(solid("gray")), "prompt": "ok"})
+        assert r.status_code == 200

@@ -14,7 +14,7 @@ for f in qwen_image_edit_streamdiffusion_amd/csrc/*.hip; do
   b=$(basename $f .hip)
   if [ -n "$ONLY" ] && [ "$b" != "$ONLY" ]; then cp $MAIN/$b.o $OUT/$b.o; continue; fi
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-function -Wno-inline-asm \
-    -Xclang -target-feature -Xclang -packed-fp32-ops "$@" \
+    ${QIE_VARIANT_BASEFLAGS--Xclang -target-feature -Xclang -packed-fp32-ops -ffp-contract=off} "$@" \
     -c $f -o $OUT/$b.o &
   pids+=($!)
 done
