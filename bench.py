@@ -24,9 +24,10 @@ The same JSON line carries, under "secondary", the like-for-like workloads of
 the reference's published numbers, each timed the same way right after the
 headline (same process, same model): "stream2-cfg" (true CFG 4.0 as
 benchmark_lightning.py:28-29 / qwen_realtime.py:247-255 run it: B = 4 rows per
-frame), "stream2-int8" (configs[3]) and, on an even number of ranks > 1,
-"stream2-cfg-pairs" (configs[4]: cond / uncond on the two ranks of a pair,
-pairs x frame shard).
+frame), "stream2-vl-per-frame" (N = 1: the headline with the prompt re-encoded
+with every frame), "stream2-int8" (configs[3]) and, on an even number of ranks
+> 1, "stream2-cfg-pairs" (configs[4]: cond / uncond on the two ranks of a
+pair, pairs x frame shard).
 
 Multi-GPU (torch.distributed.run, one process per GPU, RCCL): each rank runs
 its own stream engine on its own frames (frame shard, weak scaling); rank 0
@@ -49,6 +50,7 @@ import ctypes
 import json
 import os
 import sys
+import threading
 import time
 
 # HIP hardware queues per process, set before HIP initialises (first torch.cuda call). RCCL's own
@@ -167,6 +169,8 @@ def main():
     ap.add_argument("--no-secondary", action="store_true",
                     help="skip the secondary workloads (stream2-cfg, stream2-int8, stream2-cfg-pairs) that the "
                          "default stream2 run times after the headline")
+    ap.add_argument("--secondary-timeout", type=float, default=240.0,
+                    help="seconds the secondary workloads may take before the line is printed without them")
     ap.add_argument("--cfg-parallel", action="store_true",
                     help="workload stream2-cfg with the cond / uncond rows on the two ranks of a pair "
                          "(configs[4]); needs an even number of ranks, or one rank with --force-dist")
@@ -187,6 +191,9 @@ def main():
                          "'down=0,up=2' (qkv / out / up / down; unnamed ones unsplit)")
     ap.add_argument("--no-text-overlap", action="store_true",
                     help="A/B: run the text stream on the caller's stream, not on a second HIP stream")
+    ap.add_argument("--eager-text-post", action="store_true",
+                    help="A/B: the text stream's post-attention linears right after the attention, beside the "
+                         "image stream's persistent GEMMs (default: behind them, beside the next block's QKV)")
     ap.add_argument("--no-mod-cache", action="store_true",
                     help="recompute the timestep MLP + modulation vectors every forward (A/B switch)")
     ap.add_argument("--no-batched-mod", action="store_true",
@@ -223,6 +230,7 @@ def main():
     model.log2q_attention = not args.no_log2q
     model.batched_modulation = not args.no_batched_mod
     model.cache_modulation = not args.no_mod_cache
+    model.defer_text_post = not args.eager_text_post
     if "=" in args.text_splits:
         model.text_splits = {k: int(v) for k, v in (kv.split("=") for kv in args.text_splits.split(","))}
     else:
@@ -269,8 +277,12 @@ def main():
         raise SystemExit("--host-io needs --vae both (RGB frames in and out)")
     out_host = torch.empty(1, 1024, 1024, 3, dtype=torch.uint8).pin_memory() if host_io else None
 
-    vl = None
-    if args.vl_per_frame:  # Qwen2.5-VL-7B on the HIP path, random weights; synthetic processor outputs
+    vl_state = {}
+
+    def get_vl():
+        """Qwen2.5-VL-7B on the HIP path, random weights; synthetic processor outputs. Built once."""
+        if "vl" in vl_state:
+            return vl_state["vl"]
         from qwen_image_edit_streamdiffusion_amd.text_encoder import (QwenVLEncoder, TextEncoderConfig,
                                                                       random_state_dict, text_state_dict_shapes)
         from qwen_image_edit_streamdiffusion_amd.vision import VisionConfig, vision_state_dict_shapes
@@ -286,11 +298,13 @@ def main():
         ids[70:70 + 196] = enc_vl.image_token_id
         gv = torch.Generator(device=dev).manual_seed(6)
         pvs = [torch.randn(28 * 28, vc.patch_dim, generator=gv, device=dev) for _ in range(nf)]
-        vl = (enc_vl, ids, pvs, [(1, 28, 28)])
+        vl_state["vl"] = (enc_vl, ids, pvs, [(1, 28, 28)])
+        return vl_state["vl"]
 
-    def run(workload: str, steps: int, warmup: int, probe: bool):
+    def run(workload: str, steps: int, warmup: int, probe: bool, vl_on: bool = False):
         """Time `steps` steps of one workload on this rank's frames; returns its result dict
-        (rank 0) with the whole-job value."""
+        (rank 0) with the whole-job value. vl_on: re-encode the prompt with every frame."""
+        vl = get_vl() if vl_on else None
         int8 = workload == "stream2-int8"
         cfg_pairs = workload == "stream2-cfg-pairs"
         cfg_on = workload in ("stream2-cfg", "stream2-cfg-pairs")
@@ -455,30 +469,12 @@ def main():
         }
 
     wl = "stream2-cfg-pairs" if args.cfg_parallel else args.workload
-    res = run(wl, args.steps, args.warmup, not args.no_probe)
+    res = run(wl, args.steps, args.warmup, not args.no_probe, args.vl_per_frame)
 
-    secondary = {}
-    if args.workload == "stream2" and not args.no_secondary and not args.vl_per_frame and not host_io:
-        names = ["stream2-cfg"]
-        if pair_group is not None and world > 1:
-            names.append("stream2-cfg-pairs")
-        names.append("stream2-int8")  # last: it quantises the model's linears
-        for name in names:
-            r = run(name, args.steps, min(args.warmup, 2), not args.no_probe)
-            secondary[name] = {k: r[k] for k in ("value", "unit", "ms_per_step", "sec_per_image", "dtype",
-                                                 "mfma_util", "tflops_per_gpu", "roofline", "config")}
-
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        try:
-            cpu = cpu_baseline()
-        except Exception as e:  # reported, never fatal to the GPU number
-            cpu = {"error": repr(e)}
-
-    if rank == 0:
+    def emit(secondary, cpu):
         line = {
             "metric": "images/sec, 1024x1024 2-step Lightning edit (" +
-                      ("Qwen2.5-VL prompt encode + " if vl is not None else "") +
+                      ("Qwen2.5-VL prompt encode + " if args.vl_per_frame else "") +
                       ("VAE encode + " if encode else "") + "DiT denoise" + (" + VAE decode" if decode else "") +
                       (", PCIe-inclusive: pinned host RGB in/out)" if host_io else ")"),
             "value": res["value"], "unit": "images/sec", "n_gpus": world, "steps": args.steps,
@@ -496,7 +492,58 @@ def main():
             "secondary": secondary or None,
         }
         print(json.dumps(line), flush=True)
+
+    # The secondary workloads must never cost the headline: every rank arms a timer before them;
+    # if they have not finished by then (a rank that died, a collective that never completes),
+    # rank 0 prints the line with what it has and every rank leaves without waiting for the rest.
+    secondary = {}
+    finished = threading.Event()
+
+    def watchdog():
+        if finished.wait(args.secondary_timeout):
+            return
+        if rank == 0:
+            secondary.setdefault("error", f"secondary workloads not finished after {args.secondary_timeout:g} s; "
+                                          "abandoned")
+            emit(dict(secondary), None)
+        sys.stdout.flush()
+        os._exit(0)
+
+    if args.workload == "stream2" and not args.no_secondary and not args.vl_per_frame and not host_io:
+        threading.Thread(target=watchdog, daemon=True).start()
+        names = ["stream2-cfg"]
+        if pair_group is not None and world > 1:
+            names.append("stream2-cfg-pairs")
+        if world == 1:
+            names.append("stream2-vl-per-frame")  # the headline with the prompt re-encoded per frame
+        names.append("stream2-int8")  # last: it quantises the model's linears
+        for name in names:
+            try:
+                if name == "stream2-vl-per-frame":
+                    r = run("stream2", args.steps, min(args.warmup, 2), not args.no_probe, True)
+                else:
+                    r = run(name, args.steps, min(args.warmup, 2), not args.no_probe)
+                secondary[name] = {k: r[k] for k in ("value", "unit", "ms_per_step", "sec_per_image", "dtype",
+                                                     "mfma_util", "tflops_per_gpu", "roofline", "config")}
+            except Exception as e:  # reported, never fatal to the headline (the watchdog covers the peers)
+                secondary[name] = {"error": repr(e)}
+                if dist_on:
+                    break  # the ranks are out of step now: no further collectives
+
+    finished.set()
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            cpu = cpu_baseline()
+        except Exception as e:  # reported, never fatal to the GPU number
+            cpu = {"error": repr(e)}
+
+    if rank == 0:
+        emit(secondary, cpu)
     if dist_on:
+        if any("error" in v for v in secondary.values() if isinstance(v, dict)):
+            sys.stdout.flush()
+            os._exit(0)  # a secondary workload failed mid-way: the group may not tear down cleanly
         dist.destroy_process_group()
 
 

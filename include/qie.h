@@ -287,9 +287,11 @@ int qie_conv2d_bf16(const void* x, int H_in, int W_in, int C, int mode, int ksiz
                     const void* bias, const void* resid, void* y, int N, qie_stream_t stream);
 
 /* qie_conv2d_bf16 (no residual) followed by QwenImageRMS_norm (+ SiLU when silu != 0) of its output
- * with `gamma` [N] (the VAE ResidualBlock's conv1 + norm2, rounding points of
+ * with `gamma` [N] (the VAE ResidualBlock's conv1 + norm2, the bf16 rounding points of
  * qie_vae_rms_norm_bf16): fused into the convolution's epilogue where one wave holds every output
- * channel of a pixel (N = 96 on the halo-tiled kernel), otherwise the two launches. */
+ * channel of a pixel (N = 96 on the halo-tiled kernel), otherwise the two launches. The fused form
+ * divides through a reciprocal with one correction step and sums the squares in another order, so
+ * it agrees with the two-launch form to within one bf16 ulp, not bit for bit. */
 int qie_conv2d_rmsnorm_bf16(const void* x, int H_in, int W_in, int C, int mode, int ksize, const void* w,
                             int64_t ldw, const void* bias, const void* gamma, int silu, void* y, int N,
                             qie_stream_t stream);

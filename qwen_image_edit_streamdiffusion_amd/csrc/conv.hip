@@ -520,8 +520,10 @@ __global__ void __launch_bounds__(256, 1)
         ss += __shfl_xor(ss, 16, 64);
         ss += __shfl_xor(ss, 32, 64);
         const float d = fmaxf(rbf(sqrtf(ss)), 1e-12f);
-        // v / d correctly rounded from one reciprocal: q = v * (1/d), then one residual step
-        // q + (v - q d) / d (exact for these normal-range operands, 3 VALU instead of ~10 per value)
+        // v / d from one reciprocal: q = v * (1/d), then one residual step q + (v - q d) / d
+        // (3 VALU instead of ~10 per value). Close to, not guaranteed equal to, the correctly
+        // rounded quotient rms_norm_kernel computes, and the sum of squares runs in another order:
+        // the fused result is within one bf16 ulp of the two-launch path, not bitwise equal to it
         const float rd = __builtin_amdgcn_rcpf(d);
 #pragma unroll
         for (int j = 0; j < 6; ++j) {

@@ -197,6 +197,15 @@ class QwenImageTransformer2DModel(nn.Module):
         # HIP stream beside the image stream; the two only meet at the joint attention (see
         # _block). False: everything on the caller's stream, in the same order (A/B switch).
         self.overlap_text_stream = True
+        # With the overlap: the text stream's post-attention linears (out-proj, MLP) of block i start
+        # only once the image stream's (persistent, one work-group per CU) have finished, i.e. beside
+        # the next block's image LN1 + QKV launch, which is not persistent. A text work-group that
+        # holds a CU when a persistent grid starts makes one of its work-groups start late, and the
+        # whole launch then ends late by as much (A/B switch: False = right after the attention).
+        self.defer_text_post = True
+        # the text stream's post-attention half of the LAST block feeds nothing (the head reads the
+        # image stream only): skipped
+        self.skip_dead_text_tail = True
         # K ranges of the text-stream linears: None = ops.splitk_splits (latency-oriented), 1 =
         # one launch of full-K tiles (least CU-time: the text launches share the chip with the
         # image stream's, so what they cost is their CU-time, not their latency)
@@ -534,8 +543,10 @@ class QwenImageTransformer2DModel(nn.Module):
         side = self._side_stream() if has_txt else None
         if side is not None:  # the text stream starts from the prologue's x_txt and stemb
             side.wait_stream(torch.cuda.current_stream())
-        for blk in self.transformer_blocks:
-            self._block(blk, ws, B, S_img, S_txt, kv_len, icos, isin, tcos, tsin, eps, side)
+        last = len(self.transformer_blocks) - 1
+        for i, blk in enumerate(self.transformer_blocks):
+            self._block(blk, ws, B, S_img, S_txt, kv_len, icos, isin, tcos, tsin, eps, side,
+                        txt_post=not (self.skip_dead_text_tail and i == last))
         if side is not None:  # the next forward's prologue rewrites x_txt
             torch.cuda.current_stream().wait_stream(side)
         # ---- head: AdaLayerNormContinuous (scale first; emb_out from the prologue) + proj_out
@@ -551,13 +562,13 @@ class QwenImageTransformer2DModel(nn.Module):
         return self._side
 
     def _block(self, blk: _Block, ws: _Workspace, B, S_img, S_txt, kv_len, icos, isin, tcos, tsin, eps,
-               side: Optional[torch.cuda.Stream] = None):
+               side: Optional[torch.cuda.Stream] = None, txt_post: bool = True):
         """One dual-stream block. The image and text streams are independent except at the
         joint attention, so with ``side`` the text stream's kernels go to that HIP stream:
           side: mod_txt, LN1, QKV (text rows of qkv), QK-norm+RoPE  -> joins main before attention
           main: mod_img, LN1, QKV (image rows of qkv), QK-norm+RoPE, [join] attention
-          side: [fork after attention] out-proj, LN2, MLP of the text stream
           main: out-proj, LN2, MLP of the image stream
+          side: [fork after the image MLP, or after the attention] out-proj, LN2, MLP of the text stream
         Each stream writes only its own buffers (x/h/att/mlp/mod/split-K workspace, disjoint row
         ranges of qkv); att_txt and the qkv text rows change hands at the join/fork, and the
         next block's attention waits for the side stream's next QKV, which follows this block's
@@ -585,9 +596,16 @@ class QwenImageTransformer2DModel(nn.Module):
             ops.attention(ws.qkv, kv_len, ws.att_img, ws.att_txt[:R_t] if has_txt else None, S_img, S_txt,
                           workspace=ws.attn_split, log2q=self.log2q_attention)
         # ---- out-proj + gated residual, LN2 + modulate, MLP + gated residual
+        if side is not None and self.defer_text_post:
+            self._stream_post(blk, ws, img, eps)
+            if has_txt and txt_post:
+                side.wait_stream(main)  # behind the image stream's persistent GEMMs
+                with self._on(side):
+                    self._stream_post(blk, ws, txt, eps)
+            return
         if side is not None:
             side.wait_stream(main)
-        if has_txt:
+        if has_txt and txt_post:
             with self._on(side):
                 self._stream_post(blk, ws, txt, eps)
         self._stream_post(blk, ws, img, eps)

@@ -6,6 +6,7 @@ language model behind a stub of the processor's contract: a prompt-dependent tok
 image-dependent patches) and a tiny-config DiT. Checks determinism, that the prompt, the image and
 true CFG each change the result, and that the served image is exactly a direct pipeline call's."""
 import base64
+import hashlib
 import io
 
 import numpy as np
@@ -35,7 +36,7 @@ class _Processor:
 
     def __call__(self, text, images=None, return_tensors=None):
         self.calls.append((text[0], None if images is None else [im.size for im in images]))
-        body = [(ord(ch) * 7 + i) % 900 for i, ch in enumerate(text[0][-24:])]
+        body = [b * 3 for b in hashlib.sha1(text[0].encode()).digest()]  # 20 tokens < 900, from the whole text
         ids = list(range(100, 164)) + [992] + [990] * 16 + [993] + body
         out = {"input_ids": torch.tensor(ids).view(1, -1), "attention_mask": torch.ones(1, len(ids), dtype=torch.long)}
         if images:
