@@ -250,8 +250,7 @@ def main():
     deliver_group = None
     if pairs_possible and (args.cfg_parallel or (args.workload == "stream2" and not args.no_secondary and world > 1)):
         pair_group, pair_role, pair_size = parallel.make_pair_groups(world)
-        heads = list(range(0, world, pair_size))
-        deliver_group = dist.new_group(ranks=heads)
+        deliver_group, _ = parallel.make_head_group(world, pair_size)
 
     # ---- synthetic inputs, resident in HBM before timing
     g = torch.Generator(device=dev).manual_seed(44)
@@ -369,7 +368,7 @@ def main():
             if host_io:  # D2H of the finished image, ordered on the compute stream
                 out_host.copy_(out.reshape(out_host.shape), non_blocking=True)
             if dist_on:
-                dist.gather(out, gather_buf if rank == 0 else None, dst=0, group=grp)
+                parallel.deliver_to_root(out, gather_buf, True, grp)
 
         for i in range(warmup):
             r = step(i)

@@ -113,6 +113,23 @@ def make_pair_groups(world: int):
     return mine, rank % 2, 2
 
 
+def make_head_group(world: int, pair_size: int):
+    """The delivery group of a pairs x frame-shard run: the cond rank of every pair (ranks 0,
+    pair_size, 2 * pair_size, ...). Every rank must call this (torch requirement), members or not.
+    Returns (group, head_ranks)."""
+    heads = list(range(0, world, pair_size))
+    return dist.new_group(ranks=heads), heads
+
+
+def deliver_to_root(x: torch.Tensor, bufs: Optional[List[torch.Tensor]], is_head: bool = True, group=None) -> None:
+    """One finished frame per head rank to rank 0 (``bufs``: one tensor per head on rank 0, None
+    elsewhere). Ranks that are not heads (the uncond rank of a pair holds the same latents as its
+    partner) do not take part."""
+    if not is_head or not dist.is_initialized():
+        return
+    dist.gather(x, bufs if dist.get_rank() == 0 else None, dst=0, group=group)
+
+
 class CFGPairStreamDenoiser(StreamBatchDenoiser):
     """The stream-batch engine with its two CFG branches on the two ranks of a pair.
 

@@ -97,6 +97,63 @@ def _worker_cfg(rank, world, port, q):
         raise
 
 
+def _worker_pairs_x_shards(rank, world, port, q):
+    """bench.py's `stream2-cfg-pairs` collective sequence on 4 ranks = 2 pairs: pair groups, the
+    delivery group of the cond ranks, per-frame all_gather inside each pair, gather of every
+    finished frame to rank 0 over the delivery group, then the barrier and the max / sum
+    reductions over all ranks. Each pair runs its own frames; rank 0 must receive, per step, the
+    finished frame of both pairs, each equal to the oracle's sequential true-CFG result."""
+    try:
+        parallel = _init(rank, world, port)
+        from oracle_compute import OracleStreamCompute
+        R, cfg, params, pe, ne, _ = _cfg_case()
+        group, role, size = parallel.make_pair_groups(world)
+        dgroup, heads = parallel.make_head_group(world, size)
+        assert heads == [0, 2] and size == 2 and role == rank % 2
+        pe_b = parallel.broadcast_prompt(pe if rank == 0 else None, tuple(pe.shape), BF16, torch.device("cpu"))
+        assert torch.equal(pe_b, pe)
+        shard = rank // size
+        g = torch.Generator().manual_seed(100 + shard)  # both ranks of a pair draw the same frames
+        frames = [(torch.randn(1, 16, 64, generator=g).to(BF16), torch.randn(1, 16, 64, generator=g).to(BF16))
+                  for _ in range(3)]
+        eng = parallel.CFGPairStreamDenoiser(None, num_steps=2, true_cfg_scale=4.0, latent_hw=(4, 4),
+                                             cond_hw=(4, 4), compute=OracleStreamCompute(params, cfg),
+                                             role=role, group=group, group_size=size)
+        eng.set_conditions(pe_b, None, ne)
+        head = role == 0
+        got = []
+        done = 0
+        for noise, cond in frames + [(None, None)]:
+            r = eng.push(noise, cond)
+            if r is None:
+                continue
+            done += 1 if head else 0
+            bufs = [torch.empty(1, 16, 64, dtype=BF16) for _ in heads] if rank == 0 else None
+            parallel.deliver_to_root(r[1].contiguous(), bufs, head, dgroup)
+            if rank == 0:
+                got.append(bufs)
+        dist.barrier()
+        tt = torch.tensor([float(rank)], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dn = torch.tensor([float(done)], dtype=torch.float64)
+        dist.all_reduce(dn, op=dist.ReduceOp.SUM)
+        ok = tt.item() == world - 1 and dn.item() == 3 * len(heads)
+        if rank == 0:
+            shapes = [(1, 4, 4), (1, 4, 4)]
+            for hi in range(len(heads)):
+                gh = torch.Generator().manual_seed(100 + hi)
+                fr = [(torch.randn(1, 16, 64, generator=gh).to(BF16), torch.randn(1, 16, 64, generator=gh).to(BF16))
+                      for _ in range(3)]
+                for i, (noise, cond) in enumerate(fr):
+                    ref = R.denoise(params, cfg, noise, cond, pe, shapes, 2, neg_embeds=ne, true_cfg_scale=4.0)
+                    ok = ok and bool(torch.equal(got[i][hi], ref))
+            q.put(("ok", ok))
+        dist.destroy_process_group()
+    except Exception as e:
+        q.put(("err", repr(e)))
+        raise
+
+
 def _run(worker, world=2, n_msgs=1, timeout=240):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -186,3 +243,8 @@ def test_cfg_pair_engine_single_process_layouts():
     base.set_conditions(pe, None, ne)
     outs = drive(base.push, base.flush)
     assert all(torch.equal(outs[i], refs[i]) for i in range(3))
+
+
+def test_cfg_pairs_times_frame_shard_collective_sequence():
+    (st, ok), = _run(_worker_pairs_x_shards, world=4)
+    assert st == "ok" and ok
