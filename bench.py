@@ -8,7 +8,7 @@ of depth 2 (= the 2 Lightning steps), cond-only (the server's default
 use_cfg=False path, server.py:49,147-153), prompt-embed cache, 1024^2 output
 (4096 noise tokens) + 1024^2 condition image (4096 tokens) + 216 text tokens.
 One "step" = one pushed frame = one batched B=2 DiT forward + per-row Euler
-step, with the VAE on both ends (HIP, SURVEY.md §8 f1): the pushed condition
+step, with the VAE on both ends (HIP): the pushed condition
 frame arrives as a uint8 RGB 1024x1024 camera image and is VAE-encoded
 (QwenImageEncoder3d + quant_conv + normalise + pack), and the frame that
 completes is VAE-decoded to uint8 RGB (unpack + de-normalise + post_quant_conv
@@ -16,7 +16,7 @@ completes is VAE-decoded to uint8 RGB (unpack + de-normalise + post_quant_conv
 both.  In steady state every step completes one image, so images/sec =
 completed frames / time.  Synthetic inputs (randn / randint with fixed seeds)
 are resident in HBM before the timed region.  The text encoder is not on this
-path: the prompt embedding comes from the prompt cache (SURVEY.md §8 f2);
+path: the prompt embedding comes from the prompt cache;
 --vl-per-frame puts it on the path (the reference's realtime call re-encodes
 the prompt with every frame, qwen_realtime.py:247-255).
 

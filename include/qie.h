@@ -7,10 +7,9 @@
  * QwenImageTransformer2DModel [U], called at server.py:137-153,
  * qwen_realtime.py:247-255 and benchmark_lightning.py:41-49, and swapped as a
  * module at benchmark_compile.py:102-106 (`pipeline.transformer = ...`).  Each
- * entry point below names the upstream operation it replaces inside that call
- * (SURVEY.md §2D kernel table K1..K14, §8 rows a1..a18).
+ * entry point below names the upstream operation it replaces inside that call.
  *
- * Conventions (SURVEY.md §8 b):
+ * Conventions:
  *   - bf16 tensors are raw 16-bit words; every pointer is device memory owned by
  *     the caller (PyTorch caching allocator).  The library never allocates,
  *     frees or synchronises, and keeps no mutable global state.
@@ -51,13 +50,13 @@ const char* qie_strerror(int code);
  * bf16).  K % 64 == 0, N % 4 == 0, 16-byte aligned rows.
  */
 
-/* K1/K3/K9/K11 -- nn.Linear (+ FeedForward GELU(approximate="tanh")) [U]:
+/* nn.Linear (+ FeedForward GELU(approximate="tanh")) [U]:
  * attn.to_q/k/v, add_*_proj, img_mlp.net.0.proj (act=GELU), img_in, txt_in,
  * proj_out.  y = act(bf16(acc + bias)) -> bf16. */
 int qie_linear_bf16(const void* x, int64_t ldx, const void* w, const void* bias, void* y,
                     int64_t ldy, int M, int N, int K, int act, qie_stream_t stream);
 
-/* K2/K4 -- attn.to_out[0] / to_add_out / *_mlp.net.2 followed by the block's
+/* attn.to_out[0] / to_add_out / *_mlp.net.2 followed by the block's
  * gated residual `hidden = hidden + gate * out` [U] (QwenImageTransformerBlock):
  * resid[m,n] = bf16(resid + bf16(gate[b(m),n] * bf16(acc + bias))),
  * b(m) = m / rows_per_batch, gate row stride gate_bstride (elements). */
@@ -66,7 +65,7 @@ int qie_linear_gated_residual_bf16(const void* x, int64_t ldx, const void* w, co
                                    void* resid, int64_t ldr, int M, int N, int K,
                                    qie_stream_t stream);
 
-/* K1 fused -- to_q|to_k|to_v (or add_q|k|v_proj) as ONE GEMM over the packed
+/* Fused: to_q|to_k|to_v (or add_q|k|v_proj) as ONE GEMM over the packed
  * weight [3*H*Dh, K]; the epilogue scatters bf16(acc + bias) into the
  * head-major joint buffer qkv[3][batch][heads][s_pad][head_dim] at sequence
  * position seq_offset + (m % rows_per_batch) of batch m / rows_per_batch
@@ -76,7 +75,7 @@ int qie_linear_qkv_bf16(const void* x, int64_t ldx, const void* w, const void* b
                         int M, int K, int rows_per_batch, int seq_offset, int batch, int heads,
                         int head_dim, int s_pad, qie_stream_t stream);
 
-/* K5/K10 -- skinny linear for M <= 16 rows (img_mod/txt_mod Linear(3072->18432)
+/* skinny linear for M <= 16 rows (img_mod/txt_mod Linear(3072->18432)
  * on SiLU(temb), timestep_embedder linears, norm_out.linear) [U]:
  * weight-bandwidth bound, y = bf16(acc + bias). */
 int qie_gemv_bf16(const void* x, int64_t ldx, const void* w, const void* bias, void* y,
@@ -84,19 +83,19 @@ int qie_gemv_bf16(const void* x, int64_t ldx, const void* w, const void* bias, v
 
 /* ------------------------------------------------------------------ norms */
 
-/* K6 -- nn.LayerNorm(elementwise_affine=False, eps) + _modulate [U]:
+/* nn.LayerNorm(elementwise_affine=False, eps) + _modulate [U]:
  * y = bf16(bf16(bf16(LN(x)) * bf16(1 + scale[b])) + shift[b]), fp32 statistics.
  * shift/scale rows are mod_bstride elements apart per batch. */
 int qie_layernorm_modulate_bf16(const void* x, int64_t ldx, const void* shift, const void* scale,
                                 int64_t mod_bstride, int rows_per_batch, void* y, int64_t ldy,
                                 int rows, int D, float eps, qie_stream_t stream);
 
-/* K9 -- RMSNorm(D, eps, elementwise_affine=True) [U] (txt_norm):
+/* RMSNorm(D, eps, elementwise_affine=True) [U] (txt_norm):
  * y = bf16(bf16(x * rsqrt(mean(x^2) + eps)) * w). */
 int qie_rmsnorm_bf16(const void* x, const void* w, void* y, int rows, int D, float eps,
                      qie_stream_t stream);
 
-/* K7 -- attn.norm_q/norm_k (or norm_added_q/k) RMSNorm(head_dim) followed by
+/* attn.norm_q/norm_k (or norm_added_q/k) RMSNorm(head_dim) followed by
  * apply_rotary_emb_qwen(use_real=False) [U], in place on sequence rows
  * [seg_start, seg_start + seg_len) of the Q and K planes of the joint buffer.
  * cos_tab/sin_tab: fp32 [seg_len][head_dim/2] rows for that segment.
@@ -106,7 +105,7 @@ int qie_qk_norm_rope_bf16(void* qkv, int batch, int heads, int head_dim, int s_p
                           int seg_len, const void* wq, const void* wk, const float* cos_tab,
                           const float* sin_tab, float eps, float q_scale, qie_stream_t stream);
 
-/* K1 + K7 fused -- the q|k|v projection of one stream (as qie_linear_qkv_bf16) followed by
+/* Fused: the q|k|v projection of one stream (as qie_linear_qkv_bf16) followed by
  * attn.norm_q/norm_k (norm_added_q/k) RMSNorm(head_dim) and apply_rotary_emb_qwen [U] on its q
  * and k rows, with the rounding points of qie_qk_norm_rope_bf16. head_dim == 128; cos_tab /
  * sin_tab: fp32 [rows_per_batch][64] for this stream's segment. Big shapes run as ONE GEMM
@@ -120,7 +119,7 @@ int qie_linear_qkv_norm_rope_bf16(const void* x, int64_t ldx, const void* w, con
 
 /* ------------------------------------------------------------------ attention */
 
-/* K8 -- joint non-causal SDPA of QwenDoubleStreamAttnProcessor2_0 [U] over the
+/* joint non-causal SDPA of QwenDoubleStreamAttnProcessor2_0 [U] over the
  * head-major joint buffer (head_dim 128).  Keys j >= kv_len_host[b] are masked
  * (batched CFG text padding).  Query row s of batch b is written to
  * out_img[(b*s_img + s)*heads*128 + h*128 + d] for s < s_img and to
@@ -158,22 +157,22 @@ int qie_attention_fwd_log2q_bf16(const void* qkv, int batch, int heads, int s_pa
 
 /* ------------------------------------------------------------------ small ops */
 
-/* K10 -- Timesteps(dim, flip_sin_to_cos=True, downscale_freq_shift=0,
+/* Timesteps(dim, flip_sin_to_cos=True, downscale_freq_shift=0,
  * scale=1000) [U]: t bf16 [batch] -> bf16 [batch, dim] = [cos | sin]. */
 int qie_timestep_embed_bf16(const void* t, void* out, int batch, int dim, qie_stream_t stream);
 
 /* nn.SiLU on a bf16 vector (temb -> SiLU(temb) feeding every *_mod Linear). */
 int qie_silu_bf16(const void* x, void* y, int64_t n, qie_stream_t stream);
 
-/* K12a -- true-CFG combine + per-token norm rescale of the Edit-Plus pipeline
- * [U] (SURVEY.md §8 a2): comb = u + s*(c-u); out = comb*(|c|/|comb|), all bf16
+/* true-CFG combine + per-token norm rescale of the Edit-Plus pipeline
+ * [U]: comb = u + s*(c-u); out = comb*(|c|/|comb|), all bf16
  * tensor ops, norms over the last dim C (fp32 accumulate).  Each of the `batch`
  * slices is [rows][C] contiguous; slices are *_bstride elements apart. */
 int qie_cfg_combine_bf16(const void* cond, int64_t cond_bstride, const void* uncond,
                          int64_t uncond_bstride, void* out, int64_t out_bstride, int batch, int rows,
                          int C, float scale, qie_stream_t stream);
 
-/* K12b -- FlowMatchEulerDiscreteScheduler.step [U] with per-batch-row dt
+/* FlowMatchEulerDiscreteScheduler.step [U] with per-batch-row dt
  * (stream batch: each row at its own sigma): out = bf16(x + bf16(dt[b] * v)).
  * Tensors are [batch][n] with independent batch strides (elements). */
 int qie_euler_step_bf16(const void* x, int64_t x_bstride, const void* v, int64_t v_bstride,
@@ -184,13 +183,13 @@ int qie_euler_step_bf16(const void* x, int64_t x_bstride, const void* v, int64_t
 int qie_copy_bf16(const void* src, int64_t src_bstride, void* dst, int64_t dst_bstride, int batch,
                   int64_t n, qie_stream_t stream);
 
-/* a5 -- _pack_latents / _unpack_latents [U]: [B,C,H,W] <-> [B,(H/2)(W/2),4C]. */
+/* _pack_latents / _unpack_latents [U]: [B,C,H,W] <-> [B,(H/2)(W/2),4C]. */
 int qie_pack_latents_bf16(const void* x, void* y, int batch, int C, int H, int W,
                           qie_stream_t stream);
 int qie_unpack_latents_bf16(const void* x, void* y, int batch, int C, int H, int W,
                             qie_stream_t stream);
 
-/* ------------------------------------------------------------------ int8 (a16)
+/* ------------------------------------------------------------------ int8
  * Int8Linear (README.md:136-141, absent from the snapshot; bnb LLM.int8 at
  * benchmark_int8.py:72-76 is the reference's int8 semantics): W8A8 with
  * per-output-channel weight scales and per-token dynamic activation scales,
@@ -200,7 +199,7 @@ int qie_unpack_latents_bf16(const void* x, void* y, int batch, int C, int H, int
 int qie_quantize_rows_i8(const void* x, int64_t ldx, void* q, int64_t ldq, float* scale, int rows,
                          int D, qie_stream_t stream);
 
-/* K6 + quantisation prologue fused: LayerNorm+modulate as above, emitted as
+/* Fused LayerNorm + quantisation prologue: LayerNorm+modulate as above, emitted as
  * int8 rows + fp32 per-row scales (the bf16 value is quantised). */
 int qie_layernorm_modulate_i8(const void* x, int64_t ldx, const void* shift, const void* scale,
                               int64_t mod_bstride, int rows_per_batch, void* q, int64_t ldq,
@@ -230,7 +229,7 @@ int qie_linear_qkv_norm_rope_i8(const void* xq, int64_t ldx, const float* sx, co
 
 /* ---- split-K linears for short-M shapes (the text stream, M = B * S_txt) ---------------------
  * Replaces the same diffusers linears as the entry points above (text-stream add_q/k/v_proj,
- * to_add_out, txt_mlp: transformer_qwenimage.py [U], SURVEY.md §8 a10/a13/a14) for shapes whose
+ * to_add_out, txt_mlp: transformer_qwenimage.py [U]) for shapes whose
  * output tiles cannot fill the chip (M = 432 gives 96 tiles for N = 3072). K is cut into
  * `splits` equal ranges (K must be a multiple of splits * 64 bf16 / splits * 128 int8). Each
  * range writes its partial sums to `workspace`, and a second kernel adds them in range order
@@ -269,7 +268,7 @@ int qie_linear_splitk_i8(const void* xq, int64_t ldx, const float* sx, const voi
                          int N, int K, int splits, void* workspace, int64_t workspace_bytes,
                          qie_stream_t stream);
 
-/* ------------------------------------------------------------------ VAE decoder (§8 f1)
+/* ------------------------------------------------------------------ VAE decoder
  * AutoencoderKLQwenImage.decode on one frame [U] (pipeline_qwenimage_edit_plus: unpack,
  * `latents / (1/std) + mean`, vae.decode(z)[:, :, 0], postprocess). On a single frame every
  * QwenImageCausalConv3d sees two zero frames of causal padding, so it is the 2-D convolution
@@ -363,7 +362,7 @@ int qie_vae_latents_out_bf16(const void* x, int64_t ldx, int batch, int h, int w
  * -> round(255 v) as uint8 RGB [pixels][3] (VaeImageProcessor.postprocess, output_type="pil"). */
 int qie_vae_rgb_out(const void* x, int64_t ldx, void* rgb, int64_t pixels, qie_stream_t stream);
 
-/* ------------------------------------------------------------------ prompt encoder (§8 f2)
+/* ------------------------------------------------------------------ prompt encoder
  * The Qwen2.5-VL language model of the prompt encoder (text_encoder, transformers
  * Qwen2_5_VLTextModel [U]); its projections / norms / attention products use the entry points
  * above (qie_linear*, qie_rmsnorm_bf16, qie_matmul_f32out_bf16, qie_softmax_rows_f32_bf16). */

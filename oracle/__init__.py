@@ -10,7 +10,7 @@ PARITY UNPINNED: the reference (shi3z/Qwen-Image-Edit-StreamDiffusion) holds no
 golden vectors, no asserts and no source for the hot-path arithmetic; that lives
 in the un-vendored third-party package ``diffusers`` (unpinned, README.md:49),
 which is absent from this container, as are the model weights.  The modules here
-restate the published upstream algorithm (SURVEY.md Appendix A) and are pinned
+restate the published upstream algorithm and are pinned
 only by closed-form known answers (sigma schedule, RoPE, timestep embedding) and
-by invariants; see DESIGN.md "Oracle".
+by invariants.
 """

@@ -9,13 +9,13 @@ What is restated, and where the reference invokes it:
   models/transformers/transformer_qwenimage.py], reached through
   ``QwenImageEditPlusPipeline.__call__`` at server.py:137-153,
   qwen_realtime.py:247-255, benchmark_lightning.py:41-49, and swapped as a
-  module at benchmark_compile.py:102-106.  Equations: SURVEY.md Appendix A.
+  module at benchmark_compile.py:102-106.
 * ``FlowMatchEulerDiscreteScheduler.set_timesteps/step`` + ``calculate_shift``
-  [U] (SURVEY.md §8 a4).
-* the true-CFG combine + norm rescale of the Edit-Plus pipeline [U]
-  (SURVEY.md §8 a2), switched on by ``true_cfg_scale=4.0, negative_prompt=" "``
+  [U].
+* the true-CFG combine + norm rescale of the Edit-Plus pipeline [U],
+  switched on by ``true_cfg_scale=4.0, negative_prompt=" "``
   at benchmark_lightning.py:28-29.
-* ``_pack_latents`` / ``_unpack_latents`` [U] (SURVEY.md §8 a5).
+* ``_pack_latents`` / ``_unpack_latents`` [U].
 
 Numerics: the reference runs the model in bf16 (``torch_dtype=torch.bfloat16``,
 server.py:66-69).  With ``emulate_bf16=True`` every tensor that diffusers stores
@@ -40,7 +40,7 @@ BF16 = torch.bfloat16
 # ----------------------------------------------------------------------------
 @dataclass
 class DiTConfig:
-    """Mirror of ``QwenImageTransformer2DModel.config`` (SURVEY.md §8 b)."""
+    """Mirror of ``QwenImageTransformer2DModel.config``."""
 
     patch_size: int = 2
     in_channels: int = 64
@@ -61,7 +61,7 @@ class DiTConfig:
 
 
 def tiny_config(**kw) -> DiTConfig:
-    """Small config for fast CPU/GPU parity cases (SURVEY.md §7 item 1 (i))."""
+    """Small config for fast CPU/GPU parity cases."""
     base = dict(num_layers=2, num_attention_heads=2, joint_attention_dim=128)
     base.update(kw)
     return DiTConfig(**base)
@@ -103,7 +103,7 @@ def param_shapes(cfg: DiTConfig) -> List[Tuple[str, Tuple[int, ...]]]:
 
 
 def random_params(cfg: DiTConfig, seed: int = 0, std: float = 0.02) -> Dict[str, torch.Tensor]:
-    """Seeded random init (SURVEY.md §8 d): Linear weights/biases N(0, std),
+    """Seeded random init: Linear weights/biases N(0, std),
     RMSNorm weights 1 + N(0, std); drawn in parameter order from one CPU
     generator, then rounded to bf16 (the model's storage dtype)."""
     g = torch.Generator().manual_seed(seed)
@@ -268,7 +268,7 @@ def joint_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor,
 def block_forward(params, i: int, img: torch.Tensor, txt: torch.Tensor, temb: torch.Tensor,
                   img_phase: torch.Tensor, txt_phase: torch.Tensor, cfg: DiTConfig, r: _R,
                   txt_valid: Optional[torch.Tensor] = None):
-    """QwenImageTransformerBlock.forward [U] (Block)."""
+    """QwenImageTransformerBlock.forward [U]."""
     p = f"transformer_blocks.{i}."
     D, H, Dh, eps = cfg.inner_dim, cfg.num_attention_heads, cfg.attention_head_dim, cfg.eps
     B, S_img, S_txt = img.shape[0], img.shape[1], txt.shape[1]
@@ -454,7 +454,7 @@ def denoise(params, cfg: DiTConfig, latents: torch.Tensor, cond_latents: torch.T
 
 
 def flops_per_forward(S_img: int, S_txt: int, cfg: DiTConfig = DiTConfig(), layers: Optional[int] = None) -> float:
-    """Algorithmic FLOPs of one B=1 forward (SURVEY.md §8 d formula)."""
+    """Algorithmic FLOPs of one B=1 forward."""
     D, L = cfg.inner_dim, (cfg.num_layers if layers is None else layers)
     S = S_img + S_txt
     return (L * (24 * S * D * D + 4 * S * S * D + 24 * D * D) + 2 * S_img * 64 * D

@@ -7,7 +7,7 @@ on the transformer (benchmark_int8.py:72-76, test_quantized.py:40-43); the
 README names an ``Int8Linear`` "INT8 Linear layer using cuBLAS Lt GEMM" and a
 "fused INT8 GEMM (quantize + matmul + dequantize)" (README.md:136-141) whose
 sources are absent.  BASELINE.json north_star asks for that path as a native
-int8 MFMA GEMM.  The build therefore defines W8A8 as below (SURVEY.md §8 a16)
+int8 MFMA GEMM.  The build therefore defines W8A8 as below
 and this module is its exact integer specification:
 
   weight   s_w[n] = max_k |W[n,k]| / 127          (fp32; 1.0 if the row is 0)

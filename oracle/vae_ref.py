@@ -1,9 +1,9 @@
 """CPU restatement of the Qwen-Image VAE decoder (AutoencoderKLQwenImage.decode) on one frame.
 
 TEST INFRASTRUCTURE ONLY (see oracle/__init__.py): the checker for the HIP path, never the
-product.  PARITY UNPINNED against diffusers (absent here, SURVEY.md §8 c).
+product.  PARITY UNPINNED against diffusers (absent here).
 
-What is restated, and where the reference invokes it (SURVEY.md §8 f1):
+What is restated, and where the reference invokes it:
 
 * ``QwenImageEditPlusPipeline`` decode tail [U: diffusers pipelines/qwenimage/
   pipeline_qwenimage_edit_plus.py], reached through server.py:137-153 and

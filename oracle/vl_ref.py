@@ -1,4 +1,4 @@
-"""Prompt-encoder checker (SURVEY.md §8 f2): the reference's text encoder is transformers'
+"""Prompt-encoder checker: the reference's text encoder is transformers'
 Qwen2.5-VL (un-vendored third-party code the reference pulls in through diffusers'
 QwenImageEditPlusPipeline.encode_prompt [U]; pinned here: transformers 5.15.0, importable in this
 image).  TEST INFRASTRUCTURE ONLY: this module builds small random-init instances of

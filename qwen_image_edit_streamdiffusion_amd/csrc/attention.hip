@@ -1,7 +1,7 @@
 // Joint non-causal flash attention forward, head_dim 128, bf16 in/out.
 //
-// Replaces the SDPA call of diffusers' QwenDoubleStreamAttnProcessor2_0 [U]
-// (SURVEY.md §2D K8, §8 a12): softmax(Q K^T / sqrt(128)) V over the joint
+// Replaces the SDPA call of diffusers' QwenDoubleStreamAttnProcessor2_0 [U]:
+// softmax(Q K^T / sqrt(128)) V over the joint
 // [image; text] sequence (8408 tokens at 1024^2), 31 % of DiT FLOPs.
 //
 // Layout: qkv = [3][B][H][s_pad][128] bf16 (written by the fused QKV GEMM

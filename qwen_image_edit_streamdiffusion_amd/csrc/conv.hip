@@ -1,4 +1,4 @@
-// Implicit-GEMM convolutions of the VAE (AutoencoderKLQwenImage on one frame, SURVEY.md §8 f1):
+// Implicit-GEMM convolutions of the VAE (AutoencoderKLQwenImage on one frame):
 // conv_kernel (per-tap gather, any shape) and conv_halo_kernel (halo-tiled 3x3, the big shapes),
 // on the tile / epilogue pieces of gemm_common.h.
 #include "gemm_common.h"
@@ -7,7 +7,7 @@ namespace {
 
 // ---------------------------------------------------------------------------------------------
 // Implicit-GEMM 3x3 / 1x1 convolution over NHWC bf16 activations (the VAE decoder's
-// QwenImageCausalConv3d on one frame and its Resample Conv2d, SURVEY.md §8 f1): output pixel p
+// QwenImageCausalConv3d on one frame and its Resample Conv2d): output pixel p
 // (row of the GEMM) x output channel (column), K = (tap, input channel) in [ky][kx][C] order,
 // zero padded to a multiple of 64. The X tile is gathered per lane straight from the input image
 // (one 16-byte chunk = 8 channels of one tap of one pixel per LDS-DMA lane): the shifted pixel of
@@ -220,7 +220,7 @@ __global__ void __launch_bounds__(WM * 2 * 64)
 
 // ---------------------------------------------------------------------------------------------
 // Halo-tiled 3x3 convolution (pad 1; MODE 0 same size, MODE 1 with the nearest-2x upsample folded
-// in) for the VAE's big 3x3 convolutions (SURVEY.md §8 f1). conv_kernel above gathers every tap's
+// in) for the VAE's big 3x3 convolutions. conv_kernel above gathers every tap's
 // pixels from L2 again (each input byte fetched 9 times) and runs 2-stage K tiles drained each step
 // (timing ablations: its gather alone is 35 % of the time, its MFMA skeleton tops out at 785 TF/s).
 // Here a workgroup owns TH x 32 output pixels x NT output channels:

@@ -1,8 +1,8 @@
 // MFMA GEMM family for the DiT linears: y = epilogue(x[M,K] . W[N,K]^T + bias).
 //
 // Replaces the cuBLAS(Lt) GEMMs that diffusers' nn.Linear layers run inside
-// QwenImageTransformerBlock [U] (SURVEY.md §2D K1-K4, K9, K11, K13) -- the 68.7 %
-// of DiT FLOPs that are linear (SURVEY.md §3.4).
+// QwenImageTransformerBlock [U] -- the 68.7 %
+// of DiT FLOPs that are linear.
 //
 // Kernels, all gfx950-only (cdna_hip_programming.md §5):
 //   gemm_w4p_kernel (big shapes: M, N >= 256, >= 160 tiles, aligned output) -- persistent, one
@@ -1329,7 +1329,7 @@ extern "C" int qie_matmul_f32out_bf16(const void* x, int64_t ldx, const void* w,
   return qie_last_error();
 }
 
-// Head-batched product for the prompt encoder's attention (SURVEY.md §8 f2): for z < batch,
+// Head-batched product for the prompt encoder's attention: for z < batch,
 //   y_z = x_z . w_{z / group}^T   (x_z = x + z bsx, w_g = w + g bsw, y_z = y + z bsy; elements)
 // out_f32 = 1: raw fp32 [M][N] (ldy == N) -- the scores; out_f32 = 0: bf16(x.w^T + bias) with
 // row stride ldy -- P.V into each head's column slice.

@@ -1,10 +1,10 @@
 // Row-wise normalisation kernels (HBM-bound; one wave per row, 16-byte lanes).
 //
-//  * LayerNorm(no affine) + AdaLN _modulate of QwenImageTransformerBlock [U]
-//    (SURVEY.md §2D K6, §8 a9), optionally emitting int8 + per-row scale for
-//    the Int8Linear path (a16: the quantisation prologue fused into the norm);
-//  * RMSNorm with weight (txt_norm, K9);
-//  * per-head RMSNorm(128) of q/k + complex RoPE (K7, §8 a11), in place on the
+//  * LayerNorm(no affine) + AdaLN _modulate of QwenImageTransformerBlock [U],
+//    optionally emitting int8 + per-row scale for the Int8Linear path (the
+//    quantisation prologue fused into the norm);
+//  * RMSNorm with weight (txt_norm);
+//  * per-head RMSNorm(128) of q/k + complex RoPE, in place on the
 //    head-major joint QKV buffer;
 //  * per-row int8 quantisation of GEMM inputs that are not produced by a norm
 //    (attention output, GELU output).

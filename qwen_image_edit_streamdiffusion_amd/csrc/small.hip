@@ -1,8 +1,8 @@
 // Small / bandwidth-bound kernels of the denoise loop:
-//   timestep sinusoid (K10), SiLU, true-CFG combine + norm rescale (K12a),
-//   FlowMatch Euler step with per-row dt (K12b), strided batch copy,
-//   latent pack/unpack (a5), and the skinny GEMV used for the AdaLN
-//   modulation linears (K5: img_mod/txt_mod 3072->18432 on SiLU(temb)),
+//   timestep sinusoid, SiLU, true-CFG combine + norm rescale,
+//   FlowMatch Euler step with per-row dt, strided batch copy,
+//   latent pack/unpack, and the skinny GEMV used for the AdaLN
+//   modulation linears (img_mod/txt_mod 3072->18432 on SiLU(temb)),
 //   which is weight-bandwidth bound (13.6 GB of weights per forward).
 #include "qie_common.h"
 

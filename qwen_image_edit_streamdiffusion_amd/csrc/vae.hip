@@ -1,4 +1,4 @@
-// VAE decoder (AutoencoderKLQwenImage on one frame, SURVEY.md §8 f1) -- the memory-bound pieces
+// VAE decoder (AutoencoderKLQwenImage on one frame) -- the memory-bound pieces
 // around the implicit-GEMM convolutions of gemm.hip (qie_conv2d_bf16). Activations are NHWC bf16
 // ([pixels][channels], channels contiguous), so every per-pixel channel reduction is one
 // contiguous row and every convolution is a GEMM over K = (tap, channel).

@@ -1,4 +1,4 @@
-// Flash attention for the VAE mid-block (QwenImageAttentionBlock [U], SURVEY.md §8 f1): ONE head
+// Flash attention for the VAE mid-block (QwenImageAttentionBlock [U]): ONE head
 // of C = 384 channels over the P = h*w latent pixels (16384 at 1024^2), softmax(q k^T / sqrt(C)) v.
 // Replaces the materialised form (fp32 scores [P][P] = 1 GiB at 1024^2, a row softmax to bf16,
 // then P.V): the scores never leave the registers.

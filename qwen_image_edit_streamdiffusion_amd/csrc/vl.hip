@@ -1,4 +1,4 @@
-// Qwen2.5-VL prompt-encoder pieces (SURVEY.md §8 f2): row gather (token embedding, window
+// Qwen2.5-VL prompt-encoder pieces: row gather (token embedding, window
 // permutation), rotate-half RoPE (3-D M-RoPE tables / 2-D vision tables), SwiGLU gating, erf GELU. The projections, RMSNorms and the
 // attention products run on the GEMM / norm kernels of gemm.hip / norm.hip / vae.hip.
 //

@@ -1,10 +1,10 @@
-"""Multi-GPU request dispatcher for the ``/edit`` server (SURVEY.md §8 f3).
+"""Multi-GPU request dispatcher for the ``/edit`` server.
 
 The reference serves one request at a time on one pinned GPU (``CUDA_VISIBLE_DEVICES='7'``,
 one-thread executor, 429 while busy: server.py:8, 39-40, 190-191). Here one worker process per
 GPU owns its own pipeline, and the server hands each request to any idle worker. It answers 429
 only when every worker is busy. Requests are independent, so nothing is exchanged between
-GPUs (the multi-GPU axis of SURVEY.md §8 e, "frames / requests round-robin").
+GPUs (the frames / requests round-robin axis of multi-GPU serving).
 
 Workers are started with the ``spawn`` method before the server process touches the GPU.
 ``start()`` refuses to run if this process has already initialised HIP: spawning re-executes

@@ -432,7 +432,7 @@ def linear_splitk_i8(xq, sx, wq, sw, b, kind: int, out: torch.Tensor, workspace:
     return out
 
 
-# ---------------------------------------------------------------------------- VAE decoder (§8 f1)
+# ---------------------------------------------------------------------------- VAE decoder
 def conv_kpad(C: int, ksize: int) -> int:
     """Row length of a conv2d weight in the [Cout][ky][kx][C] layout qie_conv2d_bf16 reads."""
     return -(-(ksize * ksize * C) // 64) * 64
@@ -645,7 +645,7 @@ def vae_latents_out(x: torch.Tensor, B: int, h: int, w: int, mean: torch.Tensor,
     return out
 
 
-# ---------------------------------------------------------------------------- prompt encoder (§8 f2)
+# ---------------------------------------------------------------------------- prompt encoder
 def embed_rows(table: torch.Tensor, ids: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     _dev(table, ids, out)
     _chk(table.dtype == BF16 and table.is_contiguous() and ids.dtype == torch.int32 and ids.is_contiguous(), "embed")

@@ -1,4 +1,4 @@
-"""Multi-GPU axes of the hot path (SURVEY.md §8 e): one process per GPU.
+"""Multi-GPU axes of the hot path: one process per GPU.
 
 * Frame shard (stream axis): frames are independent, so each rank (or each
   CFG pair) runs its own stream-batch engine on its own frames -- no collective

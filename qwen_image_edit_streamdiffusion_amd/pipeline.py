@@ -8,15 +8,15 @@ qwen_realtime.py:116-122, 247-255; benchmark_lightning.py:41-49):
 ``pipe(image=[...], prompt=..., negative_prompt=..., true_cfg_scale=4.0,
 num_inference_steps=N, guidance_scale=..., generator=...) -> .images``.
 
-What runs here is the hot path (SURVEY.md §8 a1-a5): latent prep + pack, the
-FlowMatch schedule, and the denoise loop with **batched CFG** (a3, the absent
+What runs here is the hot path: latent prep + pack, the
+FlowMatch schedule, and the denoise loop with **batched CFG** (the absent
 ``batched_cfg_pipeline.py`` of README.md:126: cond and uncond stacked on the
 batch axis in ONE forward, unequal text lengths key-masked so the result equals
-the reference's two sequential forwards), the true-CFG norm rescale (a2) and
-the Euler step, then the VAE decode (§8 f1, ``vae.QwenImageVAEDecoder``: unpack,
+the reference's two sequential forwards), the true-CFG norm rescale and
+the Euler step, then the VAE decode (``vae.QwenImageVAEDecoder``: unpack,
 de-normalise, decoder, uint8 RGB, all on the HIP path).  The condition image is
 VAE-encoded on the HIP path (``vae.QwenImageVAEEncoder``) and the prompt is encoded
-by Qwen2.5-VL on the HIP path (§8 f2, ``text_encoder.QwenImageEditPromptEncoder``
+by Qwen2.5-VL on the HIP path (``text_encoder.QwenImageEditPromptEncoder``
 behind the snapshot's processor); callers may still pass ``prompt_embeds`` /
 ``image_latents`` directly or plug their own encoders into the ``prompt_encoder`` /
 ``image_encoder`` hooks (``latent_decoder`` overrides the HIP decoder).  ``output_type="latent"`` returns packed latents, as diffusers does.
@@ -231,7 +231,7 @@ class QwenImageEditPlusPipeline:
                  negative_prompt_embeds_mask=None, image_latents=None,
                  cond_shape=None, output_type: str = "pil",
                  return_dict: bool = True, batched_cfg: bool = True, **unused):
-        # guidance_scale is a no-op for this non-guidance-distilled model [U] (SURVEY.md §0.7)
+        # guidance_scale is a no-op for this non-guidance-distilled model [U]
         dev = self.transformer.device
         if height is None or width is None:
             im = image[-1] if isinstance(image, list) else image

@@ -3,7 +3,7 @@
 Built once per (img_shapes, txt_len) on the host in fp32 exactly as diffusers
 builds its ``pos_freqs``/``neg_freqs`` (outer(index, theta^(-2j/d)) then
 polar -> cos/sin), uploaded to HBM and consumed by ``qie_qk_norm_rope_bf16``.
-SURVEY.md §8 a7; the reference invokes it through every pipeline call
+The reference invokes it through every pipeline call
 (server.py:137-153) with ``img_shapes=[[(1,64,64),(1,64,64)]]`` at 1024^2.
 """
 from __future__ import annotations

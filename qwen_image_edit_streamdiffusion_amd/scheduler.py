@@ -1,7 +1,7 @@
 """FlowMatchEulerDiscreteScheduler for the Qwen-Image pipelines [U].
 
 Host side: the sigma schedule (set_timesteps with dynamic exponential shift and
-terminal stretch, SURVEY.md §8 a4) in fp32 numpy exactly as diffusers computes
+terminal stretch) in fp32 numpy exactly as diffusers computes
 it; device side: ``step`` runs the fused Euler kernel (qie_euler_step_bf16),
 which reproduces diffusers' rounding: the 0-d fp32 ``dt`` times the bf16 model
 output gives a bf16 product, added to the fp32-cast sample, cast back to bf16.

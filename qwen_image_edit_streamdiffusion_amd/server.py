@@ -1,4 +1,4 @@
-"""``/edit`` serving surface (SURVEY.md §8 f3): a drop-in for the reference's ``server.py``.
+"""``/edit`` serving surface: a drop-in for the reference's ``server.py``.
 
 Same HTTP contract as ``server.py``:
   * ``GET /`` (name, endpoints, status), ``GET /health``, ``POST /edit`` with
@@ -149,7 +149,7 @@ def load_pipeline_from_env(device: str = "cuda"):
     ``QIE_INT8=1``: quantise the linears (W8A8) after loading;
     ``QIE_ENCODERS=module:factory``: ``factory(pipeline)`` overrides ``prompt_encoder`` /
     ``image_encoder`` / ``latent_decoder``. By default the snapshot's own VAE (``vae/``) and
-    Qwen2.5-VL prompt encoder (``text_encoder/`` + ``processor/``) run on the HIP path (§8 f1/f2).
+    Qwen2.5-VL prompt encoder (``text_encoder/`` + ``processor/``) run on the HIP path.
     """
     from .pipeline import QwenImageEditPlusPipeline
     path = os.environ.get("QIE_MODEL_PATH")

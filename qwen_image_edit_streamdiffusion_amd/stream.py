@@ -3,8 +3,8 @@
 Reference: ``StreamConfig`` (qwen_realtime.py:39-66), ``CachedConditions``
 (69-89; prompt-keyed ``is_valid`` 82-89), the never-called ``prepare_latent``
 (201-224: prev-latent + 0.05*noise, keyframe every 20) and ``process_frame``
-(226-268), which re-runs the whole diffusers pipeline per frame.  SURVEY.md
-§0.4 / §8 a18: "stream batch depth=2" is defined by the build, following
+(226-268), which re-runs the whole diffusers pipeline per frame.
+The reference holds no code for "stream batch depth=2"; it is defined here, following
 StreamDiffusion (README.md:3, 207-217).
 
 Design (MI355X-first): with N denoise steps the engine keeps N frames in
@@ -323,8 +323,8 @@ class StreamBatchDenoiser:
 class QwenRealtimePipeline:
     """API mirror of qwen_realtime.QwenRealtimePipeline on the HIP engine.
 
-    Frames are handed over as packed condition latents (the VAE encoder is the
-    §8 f1 next row; plug one in via ``image_encoder`` to accept PIL frames)."""
+    Frames are handed over as packed condition latents (plug ``vae.QwenImageVAEEncoder``
+    in via ``image_encoder`` to accept PIL frames)."""
 
     def __init__(self, config: StreamConfig, image_encoder=None, prompt_encoder=None, latent_decoder=None):
         self.config = config

@@ -1,4 +1,4 @@
-"""The prompt encoder's language model on the HIP path (first half).
+"""The prompt encoder's language model on the HIP path.
 
 The reference encodes each prompt (and its condition image) with the pipeline's ``text_encoder``,
 Qwen2.5-VL-7B [U: diffusers QwenImageEditPlusPipeline.encode_prompt -> transformers
@@ -388,8 +388,8 @@ def condition_size(width: int, height: int, area: int = CONDITION_IMAGE_AREA) ->
 
 
 class QwenImageEditPromptEncoder:
-    """``pipe.prompt_encoder`` for QwenImageEditPlusPipeline (encode_prompt's Edit-Plus form,
-    SURVEY.md Appendix A): format the template with one "Picture i" prefix per condition image,
+    """``pipe.prompt_encoder`` for QwenImageEditPlusPipeline (encode_prompt's Edit-Plus
+    form): format the template with one "Picture i" prefix per condition image,
     run the processor (tokenizer + Qwen2VLImageProcessor, as the reference does -- its vocabulary
     files come with the checkpoint), encode on the HIP path, drop the first 64 tokens.
     ``processor(text=[str], images=[PIL...], return_tensors="pt")`` must return input_ids,

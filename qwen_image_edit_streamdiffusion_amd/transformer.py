@@ -3,7 +3,7 @@
 The reference swaps this module in as ``pipeline.transformer = <module>``
 (benchmark_compile.py:102-106, benchmark_lightning_compile.py:89-93,
 test_compiled.py:39-43) and the Edit-Plus pipeline calls it once per denoise
-step per CFG branch (SURVEY.md §3.4, §8 b).  Same constructor config, same
+step per CFG branch.  Same constructor config, same
 ``forward`` signature and return convention, same diffusers state_dict names
 (``load_state_dict`` / LoRA fuse address them), plus ``.config``, ``.dtype``,
 ``.device`` and a no-op ``cache_context``.
@@ -36,7 +36,7 @@ BF16 = torch.bfloat16
 
 @dataclass
 class TransformerConfig:
-    """``QwenImageTransformer2DModel.config`` (SURVEY.md §8 b)."""
+    """``QwenImageTransformer2DModel.config``."""
 
     patch_size: int = 2
     in_channels: int = 64
@@ -150,7 +150,7 @@ class QwenImageTransformer2DModel(nn.Module):
                  axes_dims_rope: Tuple[int, int, int] = (16, 56, 56), device="cuda",
                  int8_only: bool = False):
         """``int8_only``: allocate no bf16 copy of the eight quantised block linears; the
-        weights then come from a pre-quantised file (``weights.load_int8``, SURVEY.md §8 f4)."""
+        weights then come from a pre-quantised file (``weights.load_int8``)."""
         super().__init__()
         self.config = TransformerConfig(patch_size, in_channels, out_channels, num_layers,
                                         attention_head_dim, num_attention_heads, joint_attention_dim,
@@ -221,7 +221,7 @@ class QwenImageTransformer2DModel(nn.Module):
         # all 120 modulation GEMVs as one launch before the blocks; False: one launch per block and
         # stream, inside the block (A/B switch)
         self.batched_modulation = True
-        # Modulation cache ("precompute once per (timestep, LoRA) and cache"):
+        # Modulation cache (computed once per (timesteps, weights) and kept):
         # the timestep MLP, the 120 AdaLN modulation vectors and norm_out's vector depend only on
         # the weights and the per-row timesteps, which repeat every forward in the stream-batch
         # loop. Keyed on the host copy of the timestep values (scheduler.model_timesteps tags its
@@ -330,7 +330,7 @@ class QwenImageTransformer2DModel(nn.Module):
     @torch.no_grad()
     def random_init_(self, seed: int = 0, std: float = 0.02):
         """Seeded N(0, std) init of every Linear weight/bias, 1 + N(0, std) for
-        RMSNorm weights (SURVEY.md §8 d), generated directly in HBM."""
+        RMSNorm weights, generated directly in HBM."""
         g = torch.Generator(device=self.device).manual_seed(seed)
         for n in self.diffusers_names():
             t = self._param_slot(n)
@@ -340,7 +340,7 @@ class QwenImageTransformer2DModel(nn.Module):
         self._requantize_if_needed()
         return self
 
-    # ------------------------------------------------------------------ int8 (a16)
+    # ------------------------------------------------------------------ int8
     _I8_LINEARS = ("qkv_img", "qkv_txt", "out_img", "out_txt", "up_img", "up_txt", "down_img", "down_txt")
 
     @torch.no_grad()
@@ -377,7 +377,7 @@ class QwenImageTransformer2DModel(nn.Module):
             self.quantize_int8()
 
     def int8_state_dict(self) -> Dict[str, torch.Tensor]:
-        """On-disk int8 image (SURVEY.md §8 f4): ``transformer_blocks.{i}.{linear}.q8`` (int8
+        """On-disk int8 image: ``transformer_blocks.{i}.{linear}.q8`` (int8
         [N, K]) and ``.scale`` (fp32 [N]) for the eight quantised linears, every other packed
         buffer under its own name. Block linears are stored packed (q|k|v in one [3D, D])."""
         if not self.int8:
@@ -723,7 +723,7 @@ class QwenImageTransformer2DModel(nn.Module):
 
     # ------------------------------------------------------------------ bookkeeping
     def flops_per_forward(self, S_img: int, S_txt: int, B: int = 1) -> float:
-        """Algorithmic FLOPs (SURVEY.md §8 d formula; padded rows not counted)."""
+        """Algorithmic FLOPs (2 per multiply-add of every linear and both attention products; padded rows not counted)."""
         c = self.config
         D, L = c.inner_dim, c.num_layers
         S = S_img + S_txt

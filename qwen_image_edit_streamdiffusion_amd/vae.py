@@ -1,4 +1,4 @@
-"""VAE decoder on the HIP path: AutoencoderKLQwenImage.decode for one frame (SURVEY.md §8 f1).
+"""VAE decoder on the HIP path: AutoencoderKLQwenImage.decode for one frame.
 
 Replaces the decode tail the reference reaches through ``QwenImageEditPlusPipeline.__call__``
 (server.py:137-153, qwen_realtime.py:247-255) and its dead helper ``decode_latent``
@@ -356,7 +356,7 @@ class QwenImageVAEDecoder(_VAEBlocks):
         return f + conv(d[-1], 3, 3, P)
 
 
-# ============================================================================ encoder (§8 f1)
+# ============================================================================ encoder
 def encoder_plan(cfg: VAEConfig) -> List[Tuple]:
     """QwenImageEncoder3d.down_blocks as a flat list (the diffusers ModuleList indices):
     ("res", idx, in, out) and ("down", idx, C, mode)."""
@@ -405,8 +405,8 @@ class QwenImageVAEEncoder(_VAEBlocks):
     uint8 RGB [B, H, W, 3] (device) -> image processor normalisation -> QwenImageEncoder3d
     (conv_in, down blocks with stride-2 Resamples folded into the conv gather, mid block,
     RMS_norm + SiLU + conv_out) -> quant_conv -> DiagonalGaussian mode (mu) ->
-    ``(mu - mean) / std`` -> packed latents [B, (H/16)(W/16), 64] (SURVEY.md §8 a5 / f1;
-    the reference reaches it through QwenImageEditPlusPipeline.__call__ at server.py:137-153 and
+    ``(mu - mean) / std`` -> packed latents [B, (H/16)(W/16), 64] (the
+    reference reaches it through QwenImageEditPlusPipeline.__call__ at server.py:137-153 and
     the dead helper ``encode_image`` at qwen_realtime.py:167-186). The ``downsample3d`` time_conv
     is skipped on a first frame, as upstream (its feat_cache starts empty)."""
 

@@ -1,6 +1,6 @@
-"""The prompt encoder's vision tower on the HIP path (second half).
+"""The prompt encoder's vision tower on the HIP path.
 
-The reference feeds each condition image (resized to a 384^2 area, SURVEY.md Appendix A) through
+The reference feeds each condition image (resized to a 384^2 area) through
 Qwen2.5-VL's vision transformer [U: transformers 5.15 models/qwen2_5_vl/modeling_qwen2_5_vl.py,
 Qwen2_5_VisionTransformerPretrainedModel; window / position helpers in transformers/vision_utils.py]:
 a 2x14x14 patch embedding (Conv3d with kernel == stride, i.e. one linear over 1176 inputs), the

@@ -4,9 +4,9 @@ The reference loads by hub name (server.py:64-69 ``from_pretrained(
 "Qwen/Qwen-Image-Edit-2509")``, server.py:76-79 ``load_lora_weights(
 "lightx2v/Qwen-Image-Lightning", weight_name="Qwen-Image-Edit-Lightning-4steps-
 V1.0.safetensors")``).  There is no network here, so this module reads LOCAL
-paths only (SURVEY.md §8 f4) with the safe loader (``safetensors``; never
+paths only with the safe loader (``safetensors``; never
 pickle), and fuses LoRA deltas into the packed bf16 weights at load time
-(W += scale * B @ A), so the Lightning adapters cost nothing per step (§2D K14).
+(W += scale * B @ A), so the Lightning adapters cost nothing per step.
 """
 from __future__ import annotations
 
@@ -174,7 +174,7 @@ def load_lora_file(path: str, weight_name: Optional[str] = None) -> Dict[str, to
 
 
 # ---------------------------------------------------------------------------------------------
-# Pre-quantised int8 image (SURVEY.md §8 f4; the reference quantises at start-up with
+# Pre-quantised int8 image (the reference quantises at start-up with
 # bitsandbytes, benchmark_int8.py:72-84, and has no on-disk int8 format). The image holds the
 # W8A8 weights this build computes with: int8 [N, K] + fp32 per-row scales for the eight block
 # linears (packed: q|k|v in one matrix), bf16 for everything else. Loading it allocates no bf16
@@ -241,7 +241,7 @@ def load_int8(path: str, device="cuda"):
     return model.load_int8_state_dict(sd)
 
 
-# ---------------------------------------------------------------------------- VAE (§8 f1)
+# ---------------------------------------------------------------------------- VAE
 def find_vae_files(path: str):
     """VAE safetensors of a diffusers snapshot (``vae/*.safetensors``)."""
     return sorted(glob.glob(os.path.join(path, "vae", "*.safetensors"))) if os.path.isdir(path) else []
@@ -294,7 +294,7 @@ def load_vae_encoder(path: str, device="cuda"):
         _vae_tensors(path, ("encoder.", "quant_conv.")))
 
 
-# ---------------------------------------------------------------------------- prompt encoder (§8 f2)
+# ---------------------------------------------------------------------------- prompt encoder
 def _prompt_encoder_configs(path: str):
     """(TextEncoderConfig, VisionConfig, image_token_id) from ``text_encoder/config.json`` -- the
     Qwen2_5_VLConfig of the snapshot; text fields at the top level (transformers 4.x checkpoints)

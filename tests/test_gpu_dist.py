@@ -2,7 +2,7 @@
 broadcast, per-step gather of the finished images, barriers and the max-over-ranks reduction --
 the code every N > 1 run of the driver takes -- run as a child process under torch.distributed.run
 with a 2-block model. Checks that it completes, prints one JSON line, and that the HIP hardware
-queue count the bench raises before HIP initialises (DESIGN.md §7) is what the rank ran with."""
+queue count the bench raises before HIP initialises is what the rank ran with."""
 import json
 import os
 import socket

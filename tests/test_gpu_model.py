@@ -211,7 +211,7 @@ def test_lora_fuse_matches_dense_delta(dev, tiny):
 
 
 def test_int8_image_roundtrip_bitwise(dev, tiny, tmp_path):
-    """a pre-quantised on-disk image reloads into a model that allocates no
+    """A pre-quantised on-disk image reloads into a model that allocates no
     bf16 copy of the quantised linears and computes bitwise the same forward."""
     cfg, params, _ = tiny
     from qwen_image_edit_streamdiffusion_amd import weights as W

@@ -1,4 +1,4 @@
-"""Prompt encoder language model (SURVEY.md §8 f2) on the GPU: the Qwen2.5-VL kernels of vl.hip
+"""Prompt encoder language model on the GPU: the Qwen2.5-VL kernels of vl.hip
 and the whole QwenVLTextModel vs transformers' Qwen2_5_VLTextModel (oracle/vl_ref.py; random
 weights of reduced width, bf16-representable, fp32 eager oracle).
 

@@ -1,4 +1,4 @@
-"""VAE decoder (SURVEY.md §8 f1) on the GPU: every VAE entry point of libqie vs the CPU oracle
+"""VAE decoder on the GPU: every VAE entry point of libqie vs the CPU oracle
 (oracle/vae_ref.py, which keeps the causal 3-D form), then the whole decode.
 
 Tolerances (bf16 storage, fp32 accumulation):

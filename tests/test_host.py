@@ -268,7 +268,7 @@ def test_stream_slots_fill_steady_flush(cpu_ops, steps, cfg_scale):
 
 
 def test_realtime_frame_resize_non_square():
-    """a 640x480 webcam frame goes to (width, height) with LANCZOS first
+    """A 640x480 webcam frame goes to (width, height) with LANCZOS first
     (qwen_realtime.py:239-243), then to the engine's cond size -- never 1184x896."""
     from PIL import Image
     cfg = stream.StreamConfig()

@@ -30,7 +30,7 @@ def test_calculate_shift_closed_form():
 
 @pytest.mark.parametrize("n,expected", [
     (2, [1.0, 0.02, 0.0]),
-    (4, [1.0, 0.76671, 0.45561, 0.02, 0.0]),   # SURVEY.md §8 a4
+    (4, [1.0, 0.76671, 0.45561, 0.02, 0.0]),
 ])
 def test_sigma_schedule_known_values(n, expected):
     s, t = R.sigma_schedule(n, 4096)
@@ -140,7 +140,7 @@ def test_attention_masking_equals_truncation():
 
 def test_batched_padded_text_equals_unbatched():
     """Key masking makes a padded batch row equal to running it alone
-    (the batched-CFG invariant, SURVEY.md §4 item 2)."""
+    (the batched-CFG invariant)."""
     cfg = R.tiny_config()
     p = R.random_params(cfg, seed=3)
     g = torch.Generator().manual_seed(0)
@@ -155,7 +155,7 @@ def test_batched_padded_text_equals_unbatched():
 
 def test_flops_formula():
     f = R.flops_per_forward(8192, 216)
-    assert f / 1e12 == pytest.approx(166.41, abs=0.05)  # SURVEY.md §8 d
+    assert f / 1e12 == pytest.approx(166.41, abs=0.05)  # per B=1 forward at 1024^2, S_txt = 216
 
 
 # ----------------------------------------------------------------------------- int8

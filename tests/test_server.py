@@ -1,4 +1,4 @@
-"""/edit serving surface (SURVEY.md §8 f3) against the reference's server.py contract, on the
+"""/edit serving surface against the reference's server.py contract, on the
 CPU with a stub pipeline: routes, codec (data-URL prefix, EXIF transpose, JPEG q90), request
 defaults (512x512 LANCZOS, seed 42, negative_prompt "" iff use_cfg), ref-image blend, and the
 503 / 429 / 500 behaviour; plus the two-worker process dispatcher (spawned CPU workers). The
@@ -155,7 +155,7 @@ def test_gpu_dispatcher_two_workers_cpu():
 
 
 def test_gpu_dispatcher_worker_death_is_500_and_respawned():
-    """a worker that dies mid-request fails that request with 500 (not a hang),
+    """A worker that dies mid-request fails that request with 500 (not a hang),
     is recorded in the health errors, and a fresh worker takes its slot (no permanent 429)."""
     import time
     from qwen_image_edit_streamdiffusion_amd.dispatch import GpuDispatcher

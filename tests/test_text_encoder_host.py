@@ -1,4 +1,4 @@
-"""Prompt encoder (§8 f2) host logic on the CPU: the 3-D M-RoPE tables against transformers' own
+"""Prompt encoder host logic on the CPU: the 3-D M-RoPE tables against transformers' own
 rotary embedding (oracle/vl_ref.py), the weight packing and config checks."""
 import pytest
 import torch
@@ -193,7 +193,7 @@ def test_prompt_hook_cache():
 
 
 def test_condition_image_resized_lanczos():
-    """the processor gets the condition image resized with LANCZOS (Edit-Plus'
+    """The processor gets the condition image resized with LANCZOS (Edit-Plus'
     VaeImageProcessor.resize default), not PIL's default BICUBIC."""
     import numpy as np
     from PIL import Image

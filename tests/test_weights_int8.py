@@ -1,4 +1,4 @@
-"""Pre-quantised int8 on-disk image (SURVEY.md §8 f4) on the CPU: save/load round trip,
+"""Pre-quantised int8 on-disk image on the CPU: save/load round trip,
 strict key/shape/dtype checks, and the int8_only guard. The quantisation here is the oracle's
 (tests only); the GPU round trip through the HIP quantiser is in test_gpu_model.py."""
 import pytest

@@ -21,7 +21,7 @@ import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-# image-stream kernels (round 2: the big image GEMMs run the persistent gemm_w4p_kernel, the fused QKV
+# image-stream kernels (the big image GEMMs run the persistent gemm_w4p_kernel, the fused QKV
 # gemm_w4l_kernel, the text stream's gemm_pp)
 KEYS = {"attention": "attn_pp_kernel", "mlp_up": "gemm_w4p_kernel<1, false>",
         "gated_gemm": "gemm_w4p_kernel<2, false>", "qkv_gemm": "gemm_w4l_kernel<5, false>"}

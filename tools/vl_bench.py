@@ -1,4 +1,4 @@
-"""Time the prompt encoder (SURVEY.md §8 f2) at Qwen2.5-VL-7B size on random bf16 weights: the
+"""Time the prompt encoder at Qwen2.5-VL-7B size on random bf16 weights: the
 vision tower on one 392x392 condition image (28x28 patches -> 196 image tokens) and the language
 model on the Edit-Plus prompt around it (S tokens). Prints one JSON line."""
 import argparse
