@@ -146,6 +146,9 @@ __global__ void __launch_bounds__(WM* WN * 64)
 // also applies the per-head RMSNorm (fp32 sum of squares over the head's 128 columns: the wave's
 // 64 + its partner wave's 64, exchanged through `smem`) and the RoPE rotation of q and k, with
 // the rounding points of qie_qk_norm_rope_bf16; it needs every wave of the workgroup here.
+// column pairs (of 4) whose residual loads go out together in the 128 x 128 block's gated-residual
+// epilogue: 32 VGPRs of residual per pair (2 pairs at once measured equal)
+constexpr int kGateJB = 1;
 template <int NT, int EPI, bool I8>
 __device__ __forceinline__ void ring_epilogue(typename MfmaOp<I8>::acc (&acc)[8][NT], const EpiArgs& e, int M,
                                               int N, int mrow0, int ncol0, int lane, char QIE_LDS* smem) {
@@ -423,6 +426,51 @@ __device__ __forceinline__ void ring_epilogue(typename MfmaOp<I8>::acc (&acc)[8]
       }
     }
     return;
+  }
+  if constexpr (EPI == EPI_GATE_RES && NT == 8) {
+    // the 128 x 128 block of the 4-wave kernels, rows in one batch (wave-uniform): per column pair
+    // the residual loads of all 8 row groups are issued together, ahead of that pair's stores --
+    // 4 round trips per block; in store order every 16-byte chunk would be one (x is updated in
+    // place, so hipcc keeps each load behind the stores before it). Same arithmetic as below.
+    const int b0 = min(mrow0, M - 1) / e.rows_per_batch;
+    if (b0 == min(mrow0 + 127, M - 1) / e.rows_per_batch) {
+#pragma unroll
+      for (int jq = 0; jq < 4; jq += kGateJB) {
+        u32x4_t gv[kGateJB], xv[kGateJB][8];
+#pragma unroll
+        for (int jj = 0; jj < kGateJB; ++jj) {
+          const int n = min(ncol0 + (jq + jj) * 32 + (g & 1) * 16 + (g >> 1) * 8, N - 8);
+          gv[jj] = *(const u32x4_t*)(e.gate + (int64_t)b0 * e.gate_bstride + n);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const int mc = min(mrow0 + i * 16 + fr, M - 1);
+            xv[jj][i] = *(const u32x4_t*)((const bf16_t*)e.out + (int64_t)mc * e.ldo + n);
+          }
+        }
+#pragma unroll
+        for (int jj = 0; jj < kGateJB; ++jj) {
+          const int jp = jq + jj;
+          const int n = ncol0 + jp * 32 + (g & 1) * 16 + (g >> 1) * 8;
+          const uint32_t gg[4] = {gv[jj].x, gv[jj].y, gv[jj].z, gv[jj].w};
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const int m = mrow0 + i * 16 + fr;
+            u32x2_t a = epi_pre_c<EPI, I8, NT>(cols, i, 2 * jp, acc[i][2 * jp]);
+            u32x2_t b = epi_pre_c<EPI, I8, NT>(cols, i, 2 * jp + 1, acc[i][2 * jp + 1]);
+            const auto sx = __builtin_amdgcn_permlane16_swap(a.x, b.x, false, false);
+            const auto sy = __builtin_amdgcn_permlane16_swap(a.y, b.y, false, false);
+            const uint32_t vv[4] = {sx[0], sy[0], sx[1], sy[1]};
+            const uint32_t xx[4] = {xv[jj][i].x, xv[jj][i].y, xv[jj][i].z, xv[jj][i].w};
+            uint32_t o[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+              o[k] = pack2(lo_f(xx[k]) + rbf(lo_f(gg[k]) * lo_f(vv[k])), hi_f(xx[k]) + rbf(hi_f(gg[k]) * hi_f(vv[k])));
+            if (m < M && n < N) *(u32x4_t*)((bf16_t*)e.out + (int64_t)m * e.ldo + n) = u32x4_t{o[0], o[1], o[2], o[3]};
+          }
+        }
+      }
+      return;
+    }
   }
   if constexpr (EPI != EPI_QKV_NR && EPI != EPI_PARTIAL) {
 #pragma unroll
