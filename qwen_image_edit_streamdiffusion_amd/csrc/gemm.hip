@@ -252,10 +252,15 @@ __device__ __forceinline__ void ring_epilogue(typename MfmaOp<I8>::acc (&acc)[8]
             // pass 2 reads them from LDS -- instead of 8 row-group round trips to L2 per wave, each
             // held behind the previous group's stores (possible alias with the qkv buffer)
             const int m0w = mrow0 & ~255, wave = threadIdx.x >> 6;
+            // table row of tile row r: (m0w + r) mod rows_per_batch, the division done once per tile
+            // (at most one wrap inside a tile when a batch has at least 256 rows)
+            const int mb = m0w % e.rows_per_batch, rmax = M - 1 - m0w;
 #pragma unroll 1
             for (int p = 0; p < 32; ++p) {
               const int P = wave * 32 + p, r = 2 * P + (lane >> 5), q = lane & 31;
-              const int sl = min(m0w + r, M - 1) % e.rows_per_batch;
+              const int t = mb + min(r, rmax);
+              const int sl = e.rows_per_batch >= 256 ? (t >= e.rows_per_batch ? t - e.rows_per_batch : t)
+                                                     : t % e.rows_per_batch;
               const float* src = (q < 16 ? e.rcos : e.rsin) + (int64_t)sl * 64 + (((q & 15) ^ (r & 15)) << 2);
               __builtin_amdgcn_global_load_lds((const void*)src, (QIE_LDS void*)(smem + P * 1024), 16, 0, 0);
             }
@@ -265,13 +270,17 @@ __device__ __forceinline__ void ring_epilogue(typename MfmaOp<I8>::acc (&acc)[8]
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
             const int rl0 = (mrow0 & 255) + fr;  // the lane's row in the work-group tile, row group 0
+            // row by row (its scatter address and 1/rms once), the row's four 32-column pairs
+            // inside; the two bf16 roundings of the norm on both halves of a complex pair at once
 #pragma unroll
-            for (int jp = 0; jp < 4; ++jp) {
-              const int d0 = jp * 32 + dl;
-              const uint32_t wv[4] = {wwv[jp].x, wwv[jp].y, wwv[jp].z, wwv[jp].w};
+            for (int i = 0; i < 8; ++i) {
+              const int m = mrow0 + i * 16 + fr, rl = rl0 + i * 16;
+              bf16_t* rp = row_ptr(min(m, M - 1));
+              const float ssi = ss[i];
 #pragma unroll
-              for (int i = 0; i < 8; ++i) {
-                const int m = mrow0 + i * 16 + fr, rl = rl0 + i * 16;
+              for (int jp = 0; jp < 4; ++jp) {
+                const int d0 = jp * 32 + dl;
+                const uint32_t wv[4] = {wwv[jp].x, wwv[jp].y, wwv[jp].z, wwv[jp].w};
                 const char QIE_LDS* rrow = smem + rl * 512 + (((d0 >> 3) ^ (rl & 15)) << 4);
                 const f32x4_t cs = *(const f32x4_t QIE_LDS*)rrow;
                 const f32x4_t sn = *(const f32x4_t QIE_LDS*)(rrow + 256);
@@ -280,11 +289,14 @@ __device__ __forceinline__ void ring_epilogue(typename MfmaOp<I8>::acc (&acc)[8]
                 uint32_t o[4];
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
-                  const float x0 = rbf(rbf(lo_f(w4[k]) * ss[i]) * lo_f(wv[k]));
-                  const float x1 = rbf(rbf(hi_f(w4[k]) * ss[i]) * hi_f(wv[k]));
+                  float x0 = lo_f(w4[k]) * ssi, x1 = hi_f(w4[k]) * ssi;
+                  rbf2(x0, x1);
+                  x0 *= lo_f(wv[k]);
+                  x1 *= hi_f(wv[k]);
+                  rbf2(x0, x1);
                   o[k] = pack2(__builtin_fmaf(x0, cs[k], -(x1 * sn[k])) * osc, __builtin_fmaf(x0, sn[k], x1 * cs[k]) * osc);
                 }
-                if (m < M) *(u32x4_t*)(row_ptr(m) + jp * 32) = u32x4_t{o[0], o[1], o[2], o[3]};
+                if (m < M) *(u32x4_t*)(rp + jp * 32) = u32x4_t{o[0], o[1], o[2], o[3]};
               }
             }
             return;
