@@ -329,8 +329,11 @@ __device__ __forceinline__ void ring_epilogue(typename MfmaOp<I8>::acc (&acc)[8]
               uint32_t o[4];
 #pragma unroll
               for (int k = 0; k < 4; ++k) {
-                const float x0 = rbf(rbf(lo_f(w4[k]) * ss[i]) * lo_f(wv[k]));
-                const float x1 = rbf(rbf(hi_f(w4[k]) * ss[i]) * hi_f(wv[k]));
+                float x0 = lo_f(w4[k]) * ss[i], x1 = hi_f(w4[k]) * ss[i];
+                rbf2(x0, x1);
+                x0 *= lo_f(wv[k]);
+                x1 *= hi_f(wv[k]);
+                rbf2(x0, x1);
                 o[k] = pack2(__builtin_fmaf(x0, cs[k], -(x1 * sn[k])) * osc, __builtin_fmaf(x0, sn[k], x1 * cs[k]) * osc);
               }
               if (m < M) *(u32x4_t*)(row_ptr(m) + jp * 32) = u32x4_t{o[0], o[1], o[2], o[3]};
