@@ -63,7 +63,7 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 // V live in 4-slot LDS rings filled by buffer_load...lds: V-phase t issues K(t+3) / V(t+2) and
 // ends with vmcnt(pieces just issued), so every tile has landed two phases before its first
 // read and the M-phase ends with a bare barrier; one barrier per phase.
-constexpr int kRing = 4;
+constexpr int kRing = 4;  // a power of two: slots are indexed t & (kRing - 1), tile indices are never negative
 #ifndef QIE_ATTN_MPRIO  // issue priority of a wave in its MFMA phase
 #define QIE_ATTN_MPRIO 2
 #endif
@@ -177,14 +177,14 @@ __global__ void __launch_bounds__(512) attn_pp_kernel(AttnArgs a) {
     vo[p] = row * 256 + ((c ^ ((row & 3) << 2)) << 4);
   }
   auto dmaK = [&](int t) {
-    char QIE_LDS* base = smem + (t % kRing) * kTileBytes;
+    char QIE_LDS* base = smem + (t & (kRing - 1)) * kTileBytes;
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
       attn_dma(kr, base + (wave + 8 * p) * 1024, ko[p], t * kTileBytes);
     }
   };
   auto dmaV = [&](int t) {
-    char QIE_LDS* base = smem + (kRing + t % kRing) * kTileBytes;
+    char QIE_LDS* base = smem + (kRing + (t & (kRing - 1))) * kTileBytes;
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
       attn_dma(vr, base + (wave + 8 * p) * 1024, vo[p], t * kTileBytes);
@@ -204,11 +204,11 @@ __global__ void __launch_bounds__(512) attn_pp_kernel(AttnArgs a) {
   auto opA = [&](int i, int tk, int tv) -> bf16x8_t {
     if (i < 16) {
       const int cb = i >> 3, ks = i & 7;
-      const char QIE_LDS* krow = smem + (tk % kRing) * kTileBytes + (cb * 32 + ql) * 256;
+      const char QIE_LDS* krow = smem + (tk & (kRing - 1)) * kTileBytes + (cb * 32 + ql) * 256;
       return *(const bf16x8_t QIE_LDS*)(krow + (((2 * ks + hf) ^ ksw) << 4));
     }
     const int j = i - 16, ks = j >> 2, db = j & 3;
-    const char QIE_LDS* vb = smem + (kRing + tv % kRing) * kTileBytes;
+    const char QIE_LDS* vb = smem + (kRing + (tv & (kRing - 1))) * kTileBytes;
     const int r0 = 16 * ks + 4 * hf + tr_row;
     const int chunk = (4 * db + 2 * tr_g1 + ((tri & 3) >> 1)) ^ tr_sw;
     const char QIE_LDS* p0 = vb + r0 * 256 + (chunk << 4) + tr_cb;
