@@ -174,6 +174,8 @@ def _qkv_nr_case(dev, B, rpb, H, K, off, s_pad, seed, hw):
     (2, 2048, 8, 256, 0, 2304, (32, 32)),    # 192 big tiles: the fused gemm_pp epilogue
     (1, 4096, 16, 384, 0, 4352, (32, 64)),   # 16 x 24 tiles, K = 3 tiles
     (2, 200, 2, 128, 40, 512, (10, 10)),     # small: GEMM + qie_qk_norm_rope_bf16 fallback
+    (3, 1000, 16, 256, 0, 1024, (20, 25)),   # 288 big tiles whose rows cross batch boundaries (table-row wrap)
+    (24, 200, 8, 256, 40, 256, (10, 10)),    # 228 big tiles, batches shorter than a tile (table row by modulo)
 ])
 @pytest.mark.parametrize("q_scale", [1.0, 0.12752])
 def test_qkv_norm_rope_fused(dev, B, rpb, H, K, off, s_pad, hw, q_scale):
